@@ -1,0 +1,137 @@
+"""ctypes mirror of include/rtw_gpu.h (field for field) and the library loader.
+
+The library is the in-tree librtw.so built by raytracingweekend_amd.build; a
+missing library is an error, never a silent fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("RTW_LIBRARY", PKG / "librtw.so"))
+
+RTW_ABI_VERSION = 1
+RTW_MAX_OPS = 4
+
+# enums (rtw_gpu.h)
+RTW_PRIM_SPHERE, RTW_PRIM_MOVING_SPHERE, RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XZ, RTW_PRIM_RECT_YZ = range(5)
+RTW_OP_TRANSLATE, RTW_OP_ROTATE_Y, RTW_OP_FLIP = 1, 2, 3
+RTW_ENTRY_GROUP, RTW_ENTRY_MEDIUM = 0, 1
+RTW_MAT_LAMBERTIAN, RTW_MAT_METAL, RTW_MAT_DIELECTRIC, RTW_MAT_DIFFUSE_LIGHT, RTW_MAT_ISOTROPIC = range(5)
+RTW_TEX_CONSTANT, RTW_TEX_CHECKER, RTW_TEX_NOISE = range(3)
+RTW_LIGHT_DEFAULT, RTW_LIGHT_XZ_RECT, RTW_LIGHT_SPHERE = range(3)
+RTW_RENDER_SHADED, RTW_RENDER_NORMAL = 0, 1
+RTW_BG_BLACK, RTW_BG_GRADIENT = 0, 1
+
+
+class rtw_prim(C.Structure):
+    _fields_ = [("type", C.c_int32), ("material", C.c_int32), ("flip", C.c_int32), ("entry", C.c_int32),
+                ("p", C.c_double * 10)]
+
+
+class rtw_entry(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("first_prim", C.c_int32), ("n_prims", C.c_int32), ("n_ops", C.c_int32),
+                ("op", C.c_int32 * RTW_MAX_OPS), ("phase_material", C.c_int32), ("bvh_root", C.c_int32),
+                ("op_param", (C.c_double * 3) * RTW_MAX_OPS), ("density", C.c_double), ("bounds", C.c_double * 6)]
+
+
+class rtw_bvh_node(C.Structure):
+    _fields_ = [("bmin", C.c_double * 3), ("bmax", C.c_double * 3), ("left", C.c_int32), ("right", C.c_int32),
+                ("count", C.c_int32), ("pad", C.c_int32)]
+
+
+class rtw_material(C.Structure):
+    _fields_ = [("type", C.c_int32), ("texture", C.c_int32), ("albedo", C.c_double * 3), ("fuzz", C.c_double),
+                ("ref_idx", C.c_double)]
+
+
+class rtw_texture(C.Structure):
+    _fields_ = [("type", C.c_int32), ("odd", C.c_int32), ("even", C.c_int32), ("pad", C.c_int32),
+                ("color", C.c_double * 3), ("scale", C.c_double)]
+
+
+class rtw_light(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("prim", C.c_int32)]
+
+
+class rtw_camera_desc(C.Structure):
+    _fields_ = [("origin", C.c_double * 3), ("lower_left", C.c_double * 3), ("horizontal", C.c_double * 3),
+                ("vertical", C.c_double * 3), ("u", C.c_double * 3), ("v", C.c_double * 3), ("w", C.c_double * 3),
+                ("time0", C.c_double), ("time1", C.c_double), ("lens_radius", C.c_double)]
+
+
+class rtw_scene_desc(C.Structure):
+    _fields_ = [("abi_version", C.c_int32), ("render_type", C.c_int32), ("background", C.c_int32),
+                ("n_prims", C.c_int32), ("n_entries", C.c_int32), ("n_materials", C.c_int32),
+                ("n_textures", C.c_int32), ("n_lights", C.c_int32), ("n_bvh_nodes", C.c_int32),
+                ("n_bvh_items", C.c_int32), ("world_bvh_root", C.c_int32), ("has_perlin", C.c_int32),
+                ("prims", C.POINTER(rtw_prim)), ("entries", C.POINTER(rtw_entry)),
+                ("materials", C.POINTER(rtw_material)), ("textures", C.POINTER(rtw_texture)),
+                ("lights", C.POINTER(rtw_light)), ("bvh_nodes", C.POINTER(rtw_bvh_node)),
+                ("bvh_items", C.POINTER(C.c_int32)), ("perlin_ranvec", C.POINTER(C.c_double)),
+                ("perlin_perm", C.POINTER(C.c_int32)), ("camera", rtw_camera_desc)]
+
+
+class rtw_render_params(C.Structure):
+    _fields_ = [("nx", C.c_int32), ("ny", C.c_int32), ("spp", C.c_int32), ("max_depth", C.c_int32),
+                ("seed", C.c_uint64), ("spp_begin", C.c_int32), ("spp_count", C.c_int32),
+                ("row_begin", C.c_int32), ("row_step", C.c_int32), ("accum_on_device", C.c_int32),
+                ("collect_kernel_times", C.c_int32), ("wavefront_paths", C.c_int32), ("reserved", C.c_int32)]
+
+
+class rtw_stats(C.Structure):
+    _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("iterations", C.c_uint64),
+                ("launches_intersect", C.c_uint64), ("ms_total", C.c_double), ("ms_intersect", C.c_double),
+                ("ms_shade", C.c_double), ("ms_finalize", C.c_double), ("bytes_intersect", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# exported symbols and their signatures (the C ABI of include/rtw_gpu.h)
+SIGNATURES = {
+    "rtw_device_count": (C.c_int, []),
+    "rtw_scene_upload": (C.c_int, [C.c_int, C.POINTER(rtw_scene_desc), C.POINTER(C.c_void_p)]),
+    "rtw_render_accumulate": (C.c_int, [C.c_void_p, C.POINTER(rtw_camera_desc), C.POINTER(rtw_render_params),
+                                        C.c_void_p, C.POINTER(rtw_stats)]),
+    "rtw_finalize_canvas": (None, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]),
+    "rtw_write_ppm": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
+    "rtw_scene_free": (None, [C.c_void_p]),
+    "rtw_last_error": (C.c_char_p, []),
+    "rtw_path_seed": (C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint32]),
+    "rtw_scene_builtin": (C.c_int, [C.c_char_p, C.c_double, C.c_int, C.POINTER(C.POINTER(rtw_scene_desc))]),
+    "rtw_scene_desc_free": (None, [C.POINTER(rtw_scene_desc)]),
+    "rtw_abi_version": (C.c_int, []),
+}
+
+_lib = None
+
+
+def lib():
+    """Load librtw.so (once).  Raises if the native library is missing."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"native library {LIB_PATH} is missing: build it with "
+                               f"`python -m raytracingweekend_amd.build` (there is no CPU fallback)")
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.rtw_abi_version() != RTW_ABI_VERSION:
+            raise RuntimeError("librtw.so ABI version mismatch; rebuild")
+        _lib = L
+    return _lib
+
+
+class RtwError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().rtw_last_error()
+        raise RtwError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

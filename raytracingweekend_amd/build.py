@@ -1,0 +1,103 @@
+"""Build the native pieces in-tree (no JIT cache: the .so files travel to the
+GPU box with the repository snapshot).
+
+  raytracingweekend_amd/librtw.so     HIP kernels (gfx950) + C ABI + host scene API
+  raytracingweekend_amd/rtw_render    C++ host program (the reference's main())
+  oracle/_ref/librtw_oracle.so        test-only C restatement (oracle/Makefile)
+  oracle/_ref/rtw_ref                 test-only reference harness, only where
+                                      /root/reference exists
+
+Run:  python -m raytracingweekend_amd.build [--force]
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = PKG / "_build"
+LIB = PKG / "librtw.so"
+CLI = PKG / "rtw_render"
+ARCH = os.environ.get("RTW_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+INCLUDES = [f"-I{ROOT / 'include'}", f"-I{CSRC}", f"-I{CSRC / 'host'}", f"-I{CSRC / 'host' / 'rtw'}"]
+# -ffp-contract=off: the reference's fp64 arithmetic is unfused (x86-64 g++
+# emits no FMA), parity needs the same roundings on the device.
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-variable",
+          "-Wno-unused-but-set-variable"]
+DEVICE = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+
+HOST_SOURCES = sorted((CSRC / "host").glob("*.cpp"))
+DEVICE_SOURCES = sorted(CSRC.glob("*.hip"))
+HEADERS = sorted(list(CSRC.rglob("*.h")) + [ROOT / "include" / "rtw_gpu.h"])
+
+
+def _newer(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(map(str, cmd))}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def _compile(src: Path, force: bool) -> Path:
+    obj = BUILD / (src.name + ".o")
+    if force or _newer(obj, [src, *HEADERS, Path(__file__)]):
+        if src.suffix == ".hip":
+            cmd = [HIPCC, *DEVICE, *COMMON, *INCLUDES, "-x", "hip", "-c", str(src), "-o", str(obj)]
+        else:
+            cmd = [HIPCC, *COMMON, *INCLUDES, "-c", str(src), "-o", str(obj)]
+        _run(cmd)
+    return obj
+
+
+def build_library(force: bool = False) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    srcs = DEVICE_SOURCES + HOST_SOURCES
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    if force or _newer(LIB, objs):
+        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)])
+    return LIB
+
+
+def build_cli(force: bool = False) -> Path:
+    src = CSRC / "tools" / "rtw_render.cpp"
+    if src.exists() and (force or _newer(CLI, [src, LIB, *HEADERS])):
+        _run([HIPCC, *COMMON, *INCLUDES, str(src), f"-L{PKG}", "-lrtw", f"-Wl,-rpath,$ORIGIN", "-o", str(CLI)])
+    return CLI
+
+
+def build_oracle(force: bool = False) -> None:
+    """Test-only checker (oracle/): the C restatement always; the reference
+    harness only where the reference sources exist (this container)."""
+    targets = ["port"]
+    if Path(os.environ.get("RTW_REFERENCE_DIR", "/root/reference/RayTracingWeekend")).is_dir():
+        targets.append("ref")
+    if force:
+        _run(["make", "-C", str(ROOT / "oracle"), "-B", *targets])
+    else:
+        _run(["make", "-C", str(ROOT / "oracle"), *targets])
+
+
+def build_all(force: bool = False) -> None:
+    build_library(force)
+    build_cli(force)
+    build_oracle(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print(f"built {LIB}")

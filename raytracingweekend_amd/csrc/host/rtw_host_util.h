@@ -1,0 +1,19 @@
+// rtw_host_util.h — error state and small helpers shared by the host library.
+#pragma once
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "rtw_gpu.h"
+
+// Record `msg` as this thread's last error and return `code`.
+int rtw_fail(int code, const std::string& msg);
+
+// malloc'd copy of a vector (nullptr for an empty one); freed with free().
+template <typename T>
+T* rtw_dup(const std::vector<T>& v) {
+    if (v.empty()) return nullptr;
+    T* p = static_cast<T*>(std::malloc(v.size() * sizeof(T)));
+    std::memcpy(p, v.data(), v.size() * sizeof(T));
+    return p;
+}

@@ -1,0 +1,618 @@
+// rtw_device.h — gfx950 device code of the path tracer: fp64 vector math,
+// per-path minstd_rand, primitive / group / world closest-hit, materials,
+// pdfs, textures and camera ray generation.
+//
+// Every function restates one reference function (file:line cited) with the
+// same fp64 operation order; the translation unit is compiled with
+// -ffp-contract=off so no multiply-add is fused (x86-64 g++ fuses none), and
+// fp64 division / sqrt are the IEEE correctly rounded sequences.  What can
+// differ from the host reference is the last ulp of ocml's sin/cos/pow/log
+// against glibc's ("Parity").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "rtw_gpu.h"
+
+#define RTW_D __device__ __forceinline__
+
+namespace rtwd {
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kTwoPi = 2 * kPi;                 // `2 * M_PI` (exact doubling)
+constexpr double kDblMax = 1.7976931348623157e308; // std::numeric_limits<double>::max()
+constexpr double kFltMax = 3.4028234663852886e38;  // FLT_MAX widened
+constexpr double kTMin = (double)0.001f;           // RayTracingWeekend.cpp:52 (float literal)
+constexpr double kStep = (double)0.0001f;          // hittable.h:447
+constexpr double kOneMinusUlp = 0.99999999999999989; // nextafter(1.0, 0.0)
+// generate_canonical's divisor: (double)((long double)R * R), R = 2^31 - 2
+constexpr double kCanonDiv = 4611686009837453312.0;
+constexpr double kCanonR = 2147483646.0;
+
+// ------------------------------------------------------------------ vec3
+struct d3 {
+    double x, y, z;
+};
+RTW_D d3 mk(double x, double y, double z) { return d3{x, y, z}; }
+RTW_D d3 operator+(d3 a, d3 b) { return d3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+RTW_D d3 operator-(d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+RTW_D d3 operator*(d3 a, d3 b) { return d3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+RTW_D d3 operator*(d3 a, double s) { return d3{a.x * s, a.y * s, a.z * s}; }
+RTW_D d3 operator/(d3 a, double s) { return d3{a.x / s, a.y / s, a.z / s}; }
+RTW_D d3 operator-(d3 a) { return d3{-a.x, -a.y, -a.z}; }
+RTW_D double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RTW_D double len2(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+RTW_D double len(d3 a) { return __builtin_sqrt(len2(a)); }
+RTW_D d3 cross(d3 a, d3 b) {  // vec3.h:54-59
+    return d3{a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x};
+}
+RTW_D d3 normalize(d3 v) { return v / len(v); }  // vec3.h:61-67
+RTW_D d3 ld3(const double* p) { return d3{p[0], p[1], p[2]}; }
+
+struct ray {
+    d3 o, d;
+    double t;
+};
+RTW_D d3 at(const ray& r, double t) { return r.o + r.d * t; }  // ray.h:103
+
+// ------------------------------------------------------------------ RNG
+// std::minstd_rand: x <- 48271 x mod (2^31 - 1), via the Mersenne fold.
+RTW_D uint32_t mr_next(uint32_t& s) {
+    const uint64_t p = (uint64_t)s * 48271u;
+    uint32_t r = (uint32_t)(p & 0x7fffffffu) + (uint32_t)(p >> 31);
+    if (r >= 0x7fffffffu) r -= 0x7fffffffu;
+    s = r;
+    return r;
+}
+
+// libstdc++ generate_canonical<double,53>(minstd_rand): two raw draws.
+RTW_D double canon(uint32_t& s) {
+    const double e1 = (double)(mr_next(s) - 1u);
+    const double e2 = (double)(mr_next(s) - 1u);
+    double sum = 0.0 + e1 * 1.0;
+    sum = sum + e2 * kCanonR;
+    double r = sum / kCanonDiv;
+    return r >= 1.0 ? kOneMinusUlp : r;
+}
+RTW_D double rnd01(uint32_t& s) { return canon(s) * (1.0 - 0.0) + 0.0; }
+RTW_D double rnd(uint32_t& s, double a, double b) { return a + (b - a) * rnd01(s); }  // utility.h:14-20
+
+RTW_D uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+// rtw_path_seed (include/rtw_gpu.h); seed_mix = splitmix64(seed)
+RTW_D uint32_t path_seed(uint64_t seed_mix, uint32_t pixel, uint32_t s) {
+    const uint64_t k = ((uint64_t)s << 32) ^ (uint64_t)pixel;
+    return (uint32_t)(1u + splitmix64(seed_mix ^ k) % 2147483646ull);
+}
+
+RTW_D int random_int(uint32_t& s, int a, int b) {  // utility.h:22-25
+    const int span = (int)((b - a + 1) * rnd01(s));
+    return a + ((b - a) < span ? (b - a) : span);
+}
+
+// utility.h:27-35 — vec3(U, U, U) is built right to left by g++: z, y, x.
+RTW_D d3 random_in_unit_sphere(uint32_t& s) {
+    d3 p;
+    do {
+        const double z = rnd01(s);
+        const double y = rnd01(s);
+        const double x = rnd01(s);
+        p = d3{x, y, z} * 2.0 - d3{1.0, 1.0, 1.0};
+    } while (dot(p, p) >= 1.0);
+    return p;
+}
+
+RTW_D d3 random_cosine_direction(uint32_t& s) {  // utility.h:54-67
+    const double r1 = rnd01(s);
+    const double r2 = rnd01(s);
+    const double z = __builtin_sqrt(1 - r2);
+    const double phi = kTwoPi * r1;
+    const double sq = __builtin_sqrt(r2);
+    return d3{cos(phi) * sq, sin(phi) * sq, z};
+}
+
+RTW_D d3 random_to_sphere(uint32_t& s, double radius, double dist2) {  // utility.h:69-81
+    const double r1 = rnd01(s);
+    const double r2 = rnd01(s);
+    const double z = 1 + r2 * (__builtin_sqrt(1 - radius * radius / dist2) - 1);
+    const double phi = kTwoPi * r1;
+    const double sq = __builtin_sqrt(1 - z * z);
+    return d3{cos(phi) * sq, sin(phi) * sq, z};
+}
+
+// ------------------------------------------------------------------ onb
+struct onb {
+    d3 u, v, w;
+};
+RTW_D onb onb_from_w(d3 n) {  // onb.h:32-38
+    onb b;
+    b.w = normalize(n);
+    const d3 a = (fabs(b.w.x) > 0.9) ? d3{0, 1, 0} : d3{1, 0, 0};
+    b.v = normalize(cross(b.w, a));
+    b.u = cross(b.w, b.v);
+    return b;
+}
+RTW_D d3 local(const onb& b, d3 a) { return b.u * a.x + b.v * a.y + b.w * a.z; }  // onb.h:21-24
+
+// ------------------------------------------------------------------ scene
+struct scene {
+    const rtw_prim* prims;
+    const rtw_entry* entries;
+    const rtw_material* materials;
+    const rtw_texture* textures;
+    const rtw_light* lights;
+    const rtw_bvh_node* nodes;
+    const int32_t* items;
+    const double* ranvec;
+    const int32_t* perm;
+    int32_t n_entries, n_lights, world_bvh_root, render_type, background;
+    int32_t has_media;
+    int32_t n_media;
+    const int32_t* media;  // entry indices of media, in list order
+};
+
+RTW_D bool is_sphere(int type) { return type <= RTW_PRIM_MOVING_SPHERE; }
+
+// sphere.h:22-25
+RTW_D d3 sphere_center(const rtw_prim& s, double time) {
+    const d3 c0 = ld3(s.p);
+    if (s.type != RTW_PRIM_MOVING_SPHERE) return c0;
+    const double f = (time - s.p[7]) / (s.p[8] - s.p[7]);
+    return c0 + (ld3(s.p + 4) - c0) * f;
+}
+
+// sphere.h:46-81 — returns the accepted root or a negative sentinel via ok.
+RTW_D bool sphere_t(const rtw_prim& s, const ray& r, double t_min, double t_max, double& t_out) {
+    const d3 cc = sphere_center(s, r.t);
+    const double radius = s.p[3];
+    const d3 oc = r.o - cc;
+    const double a = dot(r.d, r.d);
+    const double b = dot(oc, r.d);
+    const double c = dot(oc, oc) - radius * radius;
+    const double disc = b * b - a * c;
+    if (disc > 0) {
+        const double sq = __builtin_sqrt(disc);
+        double temp = (-b - sq) / a;
+        if (temp < t_max && temp > t_min) {
+            t_out = temp;
+            return true;
+        }
+        temp = (-b + sq) / a;
+        if (temp < t_max && temp > t_min) {
+            t_out = temp;
+            return true;
+        }
+    }
+    return false;
+}
+
+// hittable.h:149-165 / 184-200 / 241-257: plane axis k, in-plane axes a, b.
+RTW_D bool rect_t(const rtw_prim& q, const ray& r, double t0, double t1, double& t_out) {
+    double ok, od, ao, ad, bo, bd;
+    if (q.type == RTW_PRIM_RECT_XY) {
+        ok = r.o.z, od = r.d.z, ao = r.o.x, ad = r.d.x, bo = r.o.y, bd = r.d.y;
+    } else if (q.type == RTW_PRIM_RECT_XZ) {
+        ok = r.o.y, od = r.d.y, ao = r.o.x, ad = r.d.x, bo = r.o.z, bd = r.d.z;
+    } else {
+        ok = r.o.x, od = r.d.x, ao = r.o.y, ad = r.d.y, bo = r.o.z, bd = r.d.z;
+    }
+    const double t = (q.p[4] - ok) / od;
+    if (t < t0 || t > t1) return false;
+    const double a = ao + t * ad;
+    const double b = bo + t * bd;
+    if (a < q.p[0] || a > q.p[1] || b < q.p[2] || b > q.p[3]) return false;
+    t_out = t;
+    return true;
+}
+
+RTW_D bool prim_t(const rtw_prim& q, const ray& r, double t0, double t1, double& t_out) {
+    return is_sphere(q.type) ? sphere_t(q, r, t0, t1, t_out) : rect_t(q, r, t0, t1, t_out);
+}
+
+RTW_D d3 rect_normal(int type) {
+    return type == RTW_PRIM_RECT_XY ? d3{0, 0, 1} : (type == RTW_PRIM_RECT_XZ ? d3{0, 1, 0} : d3{1, 0, 0});
+}
+
+// translate::hit hittable.h:299-311, rotate_y::hit :373-404 (ray inward)
+RTW_D void op_ray_in(const rtw_entry& e, int k, ray& r) {
+    const double* q = e.op_param[k];
+    if (e.op[k] == RTW_OP_TRANSLATE) {
+        r.o = r.o - ld3(q);
+    } else if (e.op[k] == RTW_OP_ROTATE_Y) {
+        const double s = q[0], c = q[1];
+        const d3 o = r.o, d = r.d;
+        r.o.x = c * o.x - s * o.z;
+        r.o.z = s * o.x + c * o.z;
+        r.d.x = c * d.x - s * d.z;
+        r.d.z = s * d.x + c * d.z;
+    }
+}
+// ... and the record outward (p, normal), innermost op first
+RTW_D void op_rec_out(const rtw_entry& e, int k, d3& p, d3& n) {
+    const double* q = e.op_param[k];
+    if (e.op[k] == RTW_OP_TRANSLATE) {
+        p = p + ld3(q);
+    } else if (e.op[k] == RTW_OP_ROTATE_Y) {
+        const double s = q[0], c = q[1];
+        const d3 p0 = p, n0 = n;
+        p.x = c * p0.x + s * p0.z;
+        p.z = -s * p0.x + c * p0.z;
+        n.x = c * n0.x + s * n0.z;
+        n.z = -s * n0.x + c * n0.z;
+    } else if (e.op[k] == RTW_OP_FLIP) {
+        n = -n;
+    }
+}
+
+RTW_D ray entry_local_ray(const rtw_entry& e, ray r) {
+    for (int k = 0; k < e.n_ops; ++k) op_ray_in(e, k, r);
+    return r;
+}
+
+// ------------------------------------------------------------------ traversal
+// Candidate comparison that reproduces the list-order winner of
+// hittable_list::hit for a BVH (any visiting order): a candidate at the same
+// t as the best wins iff list order would have let it overwrite: a rect
+// (accepts t == t_max) beats every sphere and lower-indexed rects; among
+// spheres (strict t < t_max) the lowest index is kept.
+RTW_D bool better(double t, int idx, bool rectlike, double bt, int bidx, bool brect, bool has) {
+    if (t < bt) return true;
+    if (t != bt) return false;
+    if (rectlike) return !has || !brect || idx > bidx;
+    return has && !brect && idx < bidx;
+}
+
+struct hit_state {
+    double t;     // closest so far (the t_max of the next test)
+    int32_t prim; // winner, -1 none, <= -2 medium entry -(2+e)
+    bool rect;    // winner accepts equal t (for BVH tie order)
+};
+
+// Linear closest hit over prims [first, first+n) of one group in list order
+// (t range (t_min, closest]).  Exactly the reference comparisons.
+RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h) {
+    for (int i = 0; i < n; ++i) {
+        const rtw_prim& q = S.prims[first + i];
+        double t;
+        if (prim_t(q, r, t_min, h.t, t)) {
+            h.t = t;
+            h.prim = first + i;
+            h.rect = !is_sphere(q.type);
+        }
+    }
+}
+
+// Tie-exact test of prim `pi` against the running best, valid for ANY
+// visiting order (BVH): same acceptance ranges as the reference tests, ties
+// arbitrated by better().  A sphere is probed with an open upper bound so an
+// exact tie reaches the arbiter; its root choice is unchanged (if the near root
+// lies beyond h.t so does the far one).
+RTW_D void arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_state& h) {
+    const rtw_prim& q = S.prims[pi];
+    const bool rl = !is_sphere(q.type);
+    double t;
+    if (rl) {
+        if (!rect_t(q, r, t_min, h.t, t)) return;
+    } else {
+        if (!sphere_t(q, r, t_min, kDblMax, t) || t > h.t) return;
+    }
+    if (better(t, pi, rl, h.t, h.prim, h.rect, h.prim != -1)) {
+        h.t = t;
+        h.prim = pi;
+        h.rect = rl;
+    }
+}
+
+// Slab test against padded node bounds over a widened interval: it may keep
+// a node the exact test would drop, never the reverse.
+RTW_D bool slab(const rtw_bvh_node& nd, const d3& o, const d3& inv, double t0, double t1) {
+    double lo = t0, hi = t1;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double oa = a == 0 ? o.x : (a == 1 ? o.y : o.z);
+        const double ia = a == 0 ? inv.x : (a == 1 ? inv.y : inv.z);
+        const double ta = (nd.bmin[a] - oa) * ia, tb = (nd.bmax[a] - oa) * ia;
+        lo = fmax(lo, fmin(ta, tb));
+        hi = fmin(hi, fmax(ta, tb));
+    }
+    return lo <= hi;
+}
+
+constexpr int kStack = 48;
+
+RTW_D double widen_lo(double t) { return t > 0 ? t * 0.5 : t * 2.0 - 1e-9; }
+RTW_D double widen_hi(double t) { return t * (1 + 1e-12) + 1e-9; }
+
+// BVH over the prims of one group (items = prim indices).
+RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_state& h) {
+    const d3 inv = d3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
+    int stack[kStack];
+    int sp = 0;
+    stack[sp++] = root;
+    while (sp > 0) {
+        const rtw_bvh_node& nd = S.nodes[stack[--sp]];
+        if (!slab(nd, r.o, inv, widen_lo(t_min), widen_hi(h.t))) continue;
+        if (nd.count > 0) {
+            for (int k = 0; k < nd.count; ++k) arbitrate(S, S.items[nd.left + k], r, t_min, h);
+        } else if (sp + 2 <= kStack) {
+            stack[sp++] = nd.right;
+            stack[sp++] = nd.left;
+        }
+    }
+}
+
+RTW_D void group_closest(const scene& S, const rtw_entry& e, const ray& r, double t_min, hit_state& h) {
+    if (e.bvh_root >= 0)
+        group_bvh(S, e.bvh_root, r, t_min, h);
+    else
+        group_scan(S, e.first_prim, e.n_prims, r, t_min, h);
+}
+
+// Closest t of a medium's boundary in (t0, t1) (hittable.h:438-449); the
+// boundary is the entry's ops + group.
+RTW_D bool boundary_t(const scene& S, const rtw_entry& e, const ray& r, double t0, double t1, double& t) {
+    const ray lr = entry_local_ray(e, r);
+    hit_state h{t1, -1, false};
+    group_closest(S, e, lr, t0, h);
+    if (h.prim == -1) return false;
+    t = h.t;
+    return true;
+}
+
+// constant_medium::hit hittable.h:430-479 (at most one draw per call)
+RTW_D bool medium_t(const scene& S, const rtw_entry& e, const ray& r, double t_min, double t_max, uint32_t& rng,
+                    double& t_out) {
+    double t1, t2;
+    if (!boundary_t(S, e, r, -kDblMax, kDblMax, t1)) return false;
+    if (!boundary_t(S, e, r, t1 + kStep, kDblMax, t2)) return false;
+    if (t1 < t_min) t1 = t_min;
+    if (t2 > t_max) t2 = t_max;
+    if (t1 >= t2) return false;
+    if (t1 < 0) t1 = 0;
+    const double dl = len(r.d);
+    const double inside = (t2 - t1) * dl;
+    const double hit_distance = -(1 / e.density) * log(rnd01(rng));
+    if (hit_distance < inside) {
+        t_out = t1 + hit_distance / dl;
+        return true;
+    }
+    return false;
+}
+
+// World closest hit (hittable_list::hit hittable_list.h:11-37).  Without
+// media, one walk in list order equals the reference's two walks (every
+// primitive is deterministic; the second walk re-accepts only what the first
+// kept).  With media, the second walk can only change the result through the
+// media's fresh draws, so it re-evaluates just the media, in list order.
+template <bool MEDIA>
+RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
+    hit_state h{kDblMax, -1, false};
+    if (!MEDIA && S.world_bvh_root >= 0) {
+        const d3 inv = d3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
+        int stack[kStack];
+        int sp = 0;
+        stack[sp++] = S.world_bvh_root;
+        while (sp > 0) {
+            const rtw_bvh_node& nd = S.nodes[stack[--sp]];
+            if (!slab(nd, r.o, inv, widen_lo(kTMin), widen_hi(h.t))) continue;
+            if (nd.count > 0) {
+                for (int k = 0; k < nd.count; ++k) {
+                    const rtw_entry& e = S.entries[S.items[nd.left + k]];
+                    const ray lr = entry_local_ray(e, r);
+                    if (e.bvh_root >= 0) {
+                        group_bvh(S, e.bvh_root, lr, kTMin, h);
+                    } else {
+                        for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMin, h);
+                    }
+                }
+            } else if (sp + 2 <= kStack) {
+                stack[sp++] = nd.right;
+                stack[sp++] = nd.left;
+            }
+        }
+        return h;
+    }
+    for (int ei = 0; ei < S.n_entries; ++ei) {
+        const rtw_entry& e = S.entries[ei];
+        if (MEDIA && e.kind == RTW_ENTRY_MEDIUM) {
+            double t;
+            if (medium_t(S, e, r, kTMin, h.t, rng, t)) {
+                h.t = t;
+                h.prim = -(2 + ei);
+                h.rect = false;
+            }
+            continue;
+        }
+        if (e.n_ops == 0) {
+            if (e.bvh_root >= 0) {
+                group_bvh(S, e.bvh_root, r, kTMin, h);
+            } else {
+                group_scan(S, e.first_prim, e.n_prims, r, kTMin, h);
+            }
+        } else {
+            const ray lr = entry_local_ray(e, r);
+            if (e.bvh_root >= 0)
+                group_bvh(S, e.bvh_root, lr, kTMin, h);
+            else
+                group_scan(S, e.first_prim, e.n_prims, lr, kTMin, h);
+        }
+    }
+    if (MEDIA) {
+        for (int k = 0; k < S.n_media; ++k) {
+            const int ei = S.media[k];
+            double t;
+            if (medium_t(S, S.entries[ei], r, kTMin, h.t, rng, t)) {
+                h.t = t;
+                h.prim = -(2 + ei);
+                h.rect = false;
+            }
+        }
+    }
+    return h;
+}
+
+// Reconstruct the hit record (p, normal, material) of a winner exactly as
+// the reference produced it (leaf hit, then ops outward).
+RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d3& n, int& mat) {
+    if (h.prim <= -2) {  // constant_medium, hittable.h:469-472
+        const rtw_entry& e = S.entries[-h.prim - 2];
+        p = at(r, h.t);
+        n = d3{1, 0, 0};
+        mat = e.phase_material;
+        return;
+    }
+    const rtw_prim& q = S.prims[h.prim];
+    const rtw_entry& e = S.entries[q.entry];
+    const ray lr = entry_local_ray(e, r);
+    p = at(lr, h.t);
+    if (is_sphere(q.type)) {
+        const d3 cc = sphere_center(q, lr.t);
+        n = (p - cc) / q.p[3];
+    } else {
+        n = rect_normal(q.type);
+    }
+    if (q.flip & 1) n = -n;
+    for (int k = e.n_ops - 1; k >= 0; --k) op_rec_out(e, k, p, n);
+    mat = q.material;
+}
+
+// ------------------------------------------------------------------ textures
+RTW_D double smooth(double x) { return x * x * (3 - 2 * x); }  // noise.h:9-12
+
+RTW_D double perlin_noise(const scene& S, d3 p) {  // noise.h:89-151 (PERLIN branch)
+    const double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
+    const double u = p.x - fx, v = p.y - fy, w = p.z - fz;
+    const int i = (int)fx, j = (int)fy, k = (int)fz;
+    const double uu = smooth(u), vv = smooth(v), ww = smooth(w);
+    double accum = 0;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int idx = S.perm[(i + a) & 255] ^ S.perm[256 + ((j + b) & 255)] ^ S.perm[512 + ((k + c) & 255)];
+                const d3 g = ld3(S.ranvec + 3 * idx);
+                const d3 wv = d3{u - a, v - b, w - c};
+                accum += (a * uu + (1 - a) * (1 - uu)) * (b * vv + (1 - b) * (1 - vv)) *
+                         (c * ww + (1 - c) * (1 - ww)) * dot(g, wv);
+            }
+    return accum;
+}
+
+RTW_D double turb(const scene& S, d3 p) {  // noise.h:74-86
+    double accum = 0;
+    double weight = 1.0;
+    for (int i = 0; i < 7; ++i) {
+        accum += weight * perlin_noise(S, p);
+        weight *= 0.5f;
+        p = p * 2.0;
+    }
+    return fabs(accum);
+}
+
+RTW_D d3 texture_value(const scene& S, int id, d3 p) {
+    for (int guard = 0; guard < 8; ++guard) {
+        const rtw_texture& t = S.textures[id];
+        if (t.type == RTW_TEX_CONSTANT) return ld3(t.color);
+        if (t.type == RTW_TEX_CHECKER) {  // texture.h:38-49
+            const double sines = sin(10.0 * p.x) * sin(10.0 * p.y) * sin(10.0 * p.z);
+            id = sines < 0 ? t.odd : t.even;
+            continue;
+        }
+        // texture.h:57-68: vec3(1,1,1) * 0.5f * (1 + sin(scale*p.z + 10*turb(p)))
+        const double v = (1.0 * (double)0.5f) * (1 + sin(t.scale * p.z + 10 * turb(S, p)));
+        return d3{v, v, v};
+    }
+    return d3{0, 0, 0};
+}
+
+// ------------------------------------------------------------------ lights
+RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
+    if (L.kind == RTW_LIGHT_XZ_RECT) {  // hittable.h:208-222
+        const rtw_prim& q = S.prims[L.prim];
+        const ray r{o, v, kFltMax};
+        double t;
+        if (!rect_t(q, r, 0.001, __builtin_inf(), t)) return 0;
+        const double area = (q.p[1] - q.p[0]) * (q.p[3] - q.p[2]);
+        const double distance_squared = t * t * len2(v);
+        const double cosine = fabs(dot(v, d3{0, 1, 0}) / len(v));
+        return distance_squared / (cosine * area);
+    }
+    if (L.kind == RTW_LIGHT_SPHERE) {  // sphere.h:88-99
+        const rtw_prim& q = S.prims[L.prim];
+        const ray r{o, v, kFltMax};
+        double t;
+        if (!sphere_t(q, r, 0.001, __builtin_inf(), t)) return 0.0;
+        const double radius = q.p[3];
+        const double cos_theta_max = __builtin_sqrt(1 - radius * radius / len2(ld3(q.p) - o));
+        const double solid_angle = kTwoPi * (1.0 - cos_theta_max);
+        return 1.0 / solid_angle;
+    }
+    return 0.0;  // hittable.h:36
+}
+
+RTW_D d3 light_random(const scene& S, const rtw_light& L, d3 o, uint32_t& rng) {
+    if (L.kind == RTW_LIGHT_XZ_RECT) {  // hittable.h:224-228, z drawn first
+        const rtw_prim& q = S.prims[L.prim];
+        const double rz = rnd(rng, q.p[2], q.p[3]);
+        const double rx = rnd(rng, q.p[0], q.p[1]);
+        return d3{rx, q.p[4], rz} - o;
+    }
+    if (L.kind == RTW_LIGHT_SPHERE) {  // sphere.h:101-108
+        const rtw_prim& q = S.prims[L.prim];
+        const d3 direction = ld3(q.p) - o;
+        const double distance_squared = len2(direction);
+        const onb uvw = onb_from_w(direction);
+        return local(uvw, random_to_sphere(rng, q.p[3], distance_squared));
+    }
+    return d3{1, 0, 0};  // hittable.h:37
+}
+
+RTW_D double lights_pdf_value(const scene& S, d3 o, d3 v) {  // hittable_list.h:44-53
+    const double weight = 1.0 / (double)S.n_lights;
+    double sum = 0.0;
+    for (int i = 0; i < S.n_lights; ++i) sum += weight * light_pdf_value(S, S.lights[i], o, v);
+    return sum;
+}
+
+// ------------------------------------------------------------------ materials
+RTW_D d3 reflect(d3 v, d3 n) { return v - n * (2.0 * dot(v, n)); }  // material.h:10-13
+
+RTW_D bool refract(d3 v, d3 n, double ni_over_nt, d3& refracted) {  // material.h:17-39
+    const d3 uv = normalize(v);
+    const double dt = dot(uv, n);
+    const double disc = 1.0 - ni_over_nt * ni_over_nt * (1 - dt * dt);
+    if (disc > 0) {
+        refracted = (uv - n * dt) * ni_over_nt - n * __builtin_sqrt(disc);
+        return true;
+    }
+    return false;
+}
+
+RTW_D double schlick(double cosine, double ref_idx) {  // material.h:44-49
+    double r0 = (1 - ref_idx) / (1 + ref_idx);
+    r0 = r0 * r0;
+    return r0 + (1 - r0) * pow((1 - cosine), 5.0);
+}
+
+// ------------------------------------------------------------------ camera
+// camera::get_ray camera.h:36-50, random_in_unit_disk :61-69 (y drawn first)
+RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng) {
+    d3 p;
+    do {
+        const double y = rnd01(rng);
+        const double x = rnd01(rng);
+        p = d3{x, y, 0} * 2.0 - d3{1, 1, 0};
+    } while (dot(p, p) >= 1.0);
+    const d3 rd = p * c.lens_radius;
+    const d3 offset = ld3(c.u) * rd.x + ld3(c.v) * rd.y;
+    const double time = c.time0 + rnd01(rng) * (c.time1 - c.time0);
+    const d3 dir = ld3(c.lower_left) + ld3(c.horizontal) * s + ld3(c.vertical) * t - ld3(c.origin) - offset;
+    return ray{ld3(c.origin) + offset, normalize(dir), time};
+}
+
+}  // namespace rtwd

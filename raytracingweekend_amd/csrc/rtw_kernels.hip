@@ -1,0 +1,759 @@
+// rtw_kernels.hip — the wavefront path tracer for gfx950 and the C ABI
+// around it (include/rtw_gpu.h).
+//
+// Replaces the triple `_for` of RayTracingWeekend.cpp:211-250.  The recursion
+// of color() (RayTracingWeekend.cpp:45-160) is unrolled into an iterative
+// wavefront over a pool of in-flight paths kept as SoA arrays in HBM:
+//
+//   k_fill       camera ray-gen for the first min(P, samples) samples
+//   repeat:
+//     k_intersect  one world closest-hit query per live path   (traversal)
+//     k_shade      emission / scatter / mixture-pdf sampling per path; a
+//                  path that ends writes its radiance to its sample's slot of
+//                  the per-sample radiance planes and its pool slot is refilled
+//                  with a new camera sample from a block-aggregated queue
+//                  (__ballot + popcount prefix, one atomic per 256 paths)
+//     k_compact    (tail only, once the sample queue is drained) stream
+//                  compaction of live paths, __ballot/prefix-sum per tile
+//   k_reduce     per-pixel sum of the samples in increasing sample order
+//
+// Paths are independent (the RNG is keyed by (seed, pixel, sample)), so the
+// pool order never changes a result, only its speed.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "rtw_device.h"
+#include "host/rtw_host_util.h"
+
+using namespace rtwd;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+struct paths_t {
+    double *ox, *oy, *oz, *dx, *dy, *dz, *tm, *tr, *tg, *tb;
+    uint32_t *rng, *depth, *qid;
+};
+
+struct ctrs_t {
+    unsigned long long q_next;   // next sample index of the pass to hand out
+    unsigned long long segments; // world hit queries (live paths intersected)
+    unsigned int n;              // slots in the current pool
+    unsigned int n_out;          // compaction output count
+    unsigned int pad[4];
+};
+
+struct job_t {
+    rtw_camera_desc cam;
+    uint64_t seed_mix;   // splitmix64(seed)
+    uint32_t total;      // samples in this pass
+    uint32_t npix;       // pixels of this call (n_rows * nx)
+    int32_t nx, ny, row_begin, row_step, s_begin, max_depth;
+    double *Lr, *Lg, *Lb; // per-sample radiance, index q (pass-local sample id)
+};
+
+// pass-local sample id -> pixel (i, j) and global sample index s
+__device__ __forceinline__ void sample_coords(const job_t& J, uint32_t q, int& i, int& j, int& s) {
+    const uint32_t sl = q / J.npix;
+    const uint32_t rem = q - sl * J.npix;
+    const uint32_t k = rem / (uint32_t)J.nx;
+    i = (int)(rem - k * (uint32_t)J.nx);
+    j = J.row_begin + (int)k * J.row_step;
+    s = J.s_begin + (int)sl;
+}
+
+// Render-loop body RayTracingWeekend.cpp:227-231 for sample q: jitter,
+// camera::get_ray; throughput 1, depth = max_depth.
+__device__ __forceinline__ void raygen(const job_t& J, const paths_t& P, uint32_t slot, uint32_t q) {
+    int i, j, s;
+    sample_coords(J, q, i, j, s);
+    uint32_t rng = path_seed(J.seed_mix, (uint32_t)(j * J.nx + i), (uint32_t)s);
+    const double u = (double)(i + rnd01(rng)) / (double)J.nx;
+    const double v = (double)(j + rnd01(rng)) / (double)J.ny;
+    const ray r = camera_ray(J.cam, u, v, rng);
+    P.ox[slot] = r.o.x, P.oy[slot] = r.o.y, P.oz[slot] = r.o.z;
+    P.dx[slot] = r.d.x, P.dy[slot] = r.d.y, P.dz[slot] = r.d.z;
+    P.tm[slot] = r.t;
+    P.tr[slot] = 1.0, P.tg[slot] = 1.0, P.tb[slot] = 1.0;
+    P.rng[slot] = rng;
+    P.depth[slot] = (uint32_t)J.max_depth;
+    P.qid[slot] = q;
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(job_t J, paths_t P, ctrs_t* C, uint32_t n0) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n0) raygen(J, P, i, i);
+    if (i == 0) {
+        C->n = n0;
+        C->q_next = n0;
+    }
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+    const unsigned lane = threadIdx.x & 63;
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+// block-wide exclusive prefix of a per-lane flag; returns this lane's rank and
+// writes the block total to *total (all lanes).
+__device__ __forceinline__ uint32_t block_rank(bool flag, uint32_t* s_wave, uint32_t& total) {
+    const unsigned long long m = __ballot(flag);
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s_wave[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) {
+        const uint32_t c = s_wave[k];
+        before += (k < (int)w) ? c : 0u;
+        tot += c;
+    }
+    total = tot;
+    return before + (uint32_t)__popcll(m & lanemask_lt());
+}
+
+template <bool MEDIA>
+__global__ __launch_bounds__(kBlock) void k_intersect(scene S, paths_t P, double* __restrict__ ht,
+                                                      int32_t* __restrict__ hid, ctrs_t* C) {
+    __shared__ uint32_t s_cnt[kWaves];
+    const uint32_t n = C->n;
+    uint32_t live = 0;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        if (P.depth[i] == 0) continue;
+        const ray r{d3{P.ox[i], P.oy[i], P.oz[i]}, d3{P.dx[i], P.dy[i], P.dz[i]}, P.tm[i]};
+        uint32_t rng = MEDIA ? P.rng[i] : 0u;
+        const hit_state h = world_closest<MEDIA>(S, r, rng);
+        if (MEDIA) P.rng[i] = rng;
+        ht[i] = h.t;
+        hid[i] = h.prim;
+        ++live;
+    }
+    // one 64-bit atomic per block for the segment counter
+    for (int off = 32; off > 0; off >>= 1) live += __shfl_down(live, off, 64);
+    if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = live;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int k = 0; k < kWaves; ++k) t += s_cnt[k];
+        if (t) atomicAdd(&C->segments, t);
+    }
+}
+
+// Background of RayTracingWeekend.cpp:141-159.
+__device__ __forceinline__ d3 background(const scene& S, const d3& dir) {
+    if (S.background != RTW_BG_GRADIENT) return d3{0, 0, 0};
+    const d3 u = normalize(dir);
+    const double t = 0.5f * (u.y + 1.0);
+    return d3{1.0, 1.0, 1.0} * (1.0 - t) + d3{0.5f, 0.7f, 1.0} * t;  // lerp, vec3.h:84-87
+}
+
+// One segment of color() (RayTracingWeekend.cpp:52-159) for the path in
+// `slot`.  Returns true when the path ends (radiance in L); otherwise the
+// scattered ray / throughput / depth are written back to the slot.
+__device__ __forceinline__ bool shade_one(const scene& S, const paths_t& P, uint32_t slot, double t, int32_t prim,
+                                          d3& L) {
+    const ray r{d3{P.ox[slot], P.oy[slot], P.oz[slot]}, d3{P.dx[slot], P.dy[slot], P.dz[slot]}, P.tm[slot]};
+    const d3 thr{P.tr[slot], P.tg[slot], P.tb[slot]};
+    if (prim == -1) {
+        L = thr * background(S, r.d);
+        return true;
+    }
+    d3 p, n;
+    int mat;
+    hit_record(S, r, hit_state{t, prim, false}, p, n, mat);
+    if (S.render_type == RTW_RENDER_NORMAL) {  // :135-136
+        L = thr * (d3{0.5f, 0.5f, 0.5f} * (n + d3{1, 1, 1}));
+        return true;
+    }
+    const rtw_material& m = S.materials[mat];
+    uint32_t rng = P.rng[slot];
+    const uint32_t depth = P.depth[slot];
+    d3 dir;
+    d3 f;  // throughput factor of this bounce
+    if (m.type == RTW_MAT_DIFFUSE_LIGHT) {  // material.h:232-244: no scatter
+        L = (dot(n, r.d) > 0) ? thr * texture_value(S, m.texture, p) : d3{0, 0, 0};
+        return true;
+    } else if (m.type == RTW_MAT_METAL) {  // material.h:128-136
+        const d3 reflected = reflect(normalize(r.d), n);
+        dir = reflected + random_in_unit_sphere(rng) * m.fuzz;
+        f = ld3(m.albedo);
+    } else if (m.type == RTW_MAT_DIELECTRIC) {  // material.h:146-222
+        d3 outward;
+        double ni_over_nt, cosine;
+        const double ri = m.ref_idx;
+        if (dot(r.d, n) > 0) {
+            outward = -n;
+            ni_over_nt = ri;
+            cosine = dot(r.d, n) / len(r.d);
+            cosine = __builtin_sqrt(1 - ri * ri * (1 - cosine * cosine));
+        } else {
+            outward = n;
+            ni_over_nt = 1.0 / ri;
+            cosine = -dot(r.d, n) / len(r.d);
+        }
+        const d3 reflected = reflect(r.d, n);
+        d3 refracted{0, 0, 0};
+        const double reflect_prob = refract(r.d, outward, ni_over_nt, refracted) ? schlick(cosine, ri) : 1.0;
+        dir = (rnd01(rng) < reflect_prob) ? reflected : refracted;
+        f = d3{1.0, 1.0, 1.0};
+    } else if (m.type == RTW_MAT_ISOTROPIC) {  // material.h:257-262
+        dir = random_in_unit_sphere(rng);
+        f = texture_value(S, m.texture, p);
+    } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
+        const d3 att = texture_value(S, m.texture, p);
+        const onb uvw = onb_from_w(n);
+        double pdf_val;
+        if (S.n_lights > 0) {  // mixture_pdf(cosine_pdf, hittable_pdf(lights)) pdf.h:55-79
+            if (rnd01(rng) < 0.5) {
+                dir = local(uvw, random_cosine_direction(rng));
+            } else {
+                const int k = random_int(rng, 0, S.n_lights - 1);
+                dir = light_random(S, S.lights[k], p, rng);
+            }
+            const double c = dot(normalize(dir), uvw.w);
+            const double p0 = (c <= 0) ? 0 : c / kPi;
+            pdf_val = 0.5 * p0 + 0.5 * lights_pdf_value(S, p, dir);
+        } else {
+            dir = local(uvw, random_cosine_direction(rng));
+            const double c = dot(normalize(dir), uvw.w);
+            pdf_val = (c <= 0) ? 0 : c / kPi;
+        }
+        if (pdf_val <= 0.0) {  // :126-127 returns emitted (= 0)
+            L = d3{0, 0, 0};
+            return true;
+        }
+        const double cosine = dot(n, normalize(dir));  // material.h:115-119
+        const double spdf = cosine < 0 ? 0 : cosine / kPi;
+        f = (att * spdf) / pdf_val;
+    }
+    if (depth <= 1) {  // the next color() call has depth 0 and returns 0
+        L = d3{0, 0, 0};
+        return true;
+    }
+    const d3 nt = thr * f;
+    P.ox[slot] = p.x, P.oy[slot] = p.y, P.oz[slot] = p.z;
+    P.dx[slot] = dir.x, P.dy[slot] = dir.y, P.dz[slot] = dir.z;
+    P.tr[slot] = nt.x, P.tg[slot] = nt.y, P.tb[slot] = nt.z;
+    P.rng[slot] = rng;
+    P.depth[slot] = depth - 1;
+    return false;
+}
+
+__global__ __launch_bounds__(kBlock) void k_shade(scene S, job_t J, paths_t P, const double* __restrict__ ht,
+                                                  const int32_t* __restrict__ hid, ctrs_t* C) {
+    __shared__ uint32_t s_wave[kWaves];
+    __shared__ unsigned long long s_base;
+    const uint32_t n = C->n;
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t b = blockIdx.x * kBlock; b < n; b += stride) {
+        const uint32_t i = b + threadIdx.x;
+        bool need = false;
+        if (i < n && P.depth[i] != 0) {
+            d3 L;
+            if (shade_one(S, P, i, ht[i], hid[i], L)) {
+                const uint32_t q = P.qid[i];
+                J.Lr[q] = L.x, J.Lg[q] = L.y, J.Lb[q] = L.z;
+                need = true;
+            }
+        }
+        uint32_t total;
+        const uint32_t rank = block_rank(need, s_wave, total);
+        if (total) {
+            if (threadIdx.x == 0) s_base = atomicAdd(&C->q_next, (unsigned long long)total);
+            __syncthreads();
+            if (need) {
+                const unsigned long long q = s_base + rank;
+                if (q < J.total)
+                    raygen(J, P, i, (uint32_t)q);
+                else
+                    P.depth[i] = 0;  // queue drained: the slot goes dead
+            }
+        }
+        __syncthreads();  // s_wave / s_base reuse
+    }
+}
+
+// Tail-phase stream compaction of live slots (depth != 0) from A into B.
+__global__ __launch_bounds__(kBlock) void k_compact(paths_t A, paths_t B, ctrs_t* C) {
+    __shared__ uint32_t s_wave[kWaves];
+    __shared__ uint32_t s_base;
+    const uint32_t n = C->n;
+    for (uint32_t b = blockIdx.x * kBlock; b < n; b += gridDim.x * kBlock) {
+        const uint32_t i = b + threadIdx.x;
+        const bool live = i < n && A.depth[i] != 0;
+        uint32_t total;
+        const uint32_t rank = block_rank(live, s_wave, total);
+        if (total) {
+            if (threadIdx.x == 0) s_base = atomicAdd(&C->n_out, total);
+            __syncthreads();
+            if (live) {
+                const uint32_t o = s_base + rank;
+                B.ox[o] = A.ox[i], B.oy[o] = A.oy[i], B.oz[o] = A.oz[i];
+                B.dx[o] = A.dx[i], B.dy[o] = A.dy[i], B.dz[o] = A.dz[i];
+                B.tm[o] = A.tm[i];
+                B.tr[o] = A.tr[i], B.tg[o] = A.tg[i], B.tb[o] = A.tb[i];
+                B.rng[o] = A.rng[i], B.depth[o] = A.depth[i], B.qid[o] = A.qid[i];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_commit(ctrs_t* C) {
+    C->n = C->n_out;
+    C->n_out = 0;
+}
+
+// running[pix] += L[s][pix] for s = 0..S-1 in order (RayTracingWeekend.cpp:235-239)
+__global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ Lr, const double* __restrict__ Lg,
+                                                   const double* __restrict__ Lb, uint32_t npix, uint32_t spp,
+                                                   double* __restrict__ run) {
+    for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < npix; p += gridDim.x * kBlock) {
+        double r = run[3 * p], g = run[3 * p + 1], bl = run[3 * p + 2];
+        for (uint32_t s = 0; s < spp; ++s) {
+            const size_t q = (size_t)s * npix + p;
+            r = r + Lr[q];
+            g = g + Lg[q];
+            bl = bl + Lb[q];
+        }
+        run[3 * p] = r, run[3 * p + 1] = g, run[3 * p + 2] = bl;
+    }
+}
+
+// accum[(j*nx+i)*3+c] += run[(k*nx+i)*3+c], j = row_begin + k*row_step
+__global__ __launch_bounds__(kBlock) void k_emit(const double* __restrict__ run, uint32_t npix, int nx, int row_begin,
+                                                 int row_step, double* __restrict__ accum) {
+    for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < npix; p += gridDim.x * kBlock) {
+        const uint32_t k = p / (uint32_t)nx, i = p - k * (uint32_t)nx;
+        const size_t o = ((size_t)(row_begin + (int)k * row_step) * nx + i) * 3;
+        accum[o] += run[3 * p];
+        accum[o + 1] += run[3 * p + 1];
+        accum[o + 2] += run[3 * p + 2];
+    }
+}
+
+// ======================================================================
+// host side
+// ======================================================================
+#define HIPCHK(x)                                                                              \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess)                                                                  \
+            return rtw_fail(RTW_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_));      \
+    } while (0)
+
+uint64_t host_splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct dev_buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t n) {
+        if (n <= bytes) return RTW_OK;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipMalloc(&p, n) != hipSuccess) return rtw_fail(RTW_ERR_OOM, "hipMalloc of " + std::to_string(n) + " bytes failed");
+        bytes = n;
+        return RTW_OK;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct handle_t {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    scene S{};
+    bool media = false;
+    dev_buf scene_mem;
+    dev_buf pool[2];  // path SoA, ping-pong for compaction
+    dev_buf hits;
+    dev_buf radiance; // per-sample planes of one pass
+    dev_buf run;      // per-pixel running sums
+    dev_buf accum;    // device accum when the caller passes a host pointer
+    dev_buf ctrs;
+    ctrs_t* host_ctrs = nullptr;  // pinned
+    uint32_t pool_cap = 0;
+    int grid = 2048;
+    std::vector<hipEvent_t> events;
+};
+
+paths_t carve_paths(void* base, uint32_t cap) {
+    char* p = static_cast<char*>(base);
+    paths_t P;
+    double** d[] = {&P.ox, &P.oy, &P.oz, &P.dx, &P.dy, &P.dz, &P.tm, &P.tr, &P.tg, &P.tb};
+    for (double** x : d) {
+        *x = reinterpret_cast<double*>(p);
+        p += (size_t)cap * 8;
+    }
+    uint32_t** u[] = {&P.rng, &P.depth, &P.qid};
+    for (uint32_t** x : u) {
+        *x = reinterpret_cast<uint32_t*>(p);
+        p += (size_t)cap * 4;
+    }
+    return P;
+}
+size_t paths_bytes(uint32_t cap) { return (size_t)cap * (10 * 8 + 3 * 4); }
+
+int upload_scene(handle_t* h, const rtw_scene_desc* d) {
+    // one allocation, 256-byte aligned sub-arrays
+    std::vector<int32_t> media;
+    for (int e = 0; e < d->n_entries; ++e)
+        if (d->entries[e].kind == RTW_ENTRY_MEDIUM) media.push_back(e);
+    struct part {
+        const void* src;
+        size_t bytes;
+        size_t off;
+    };
+    std::vector<part> parts = {
+        {d->prims, sizeof(rtw_prim) * d->n_prims, 0},
+        {d->entries, sizeof(rtw_entry) * d->n_entries, 0},
+        {d->materials, sizeof(rtw_material) * d->n_materials, 0},
+        {d->textures, sizeof(rtw_texture) * d->n_textures, 0},
+        {d->lights, sizeof(rtw_light) * d->n_lights, 0},
+        {d->bvh_nodes, sizeof(rtw_bvh_node) * d->n_bvh_nodes, 0},
+        {d->bvh_items, sizeof(int32_t) * d->n_bvh_items, 0},
+        {d->has_perlin ? d->perlin_ranvec : nullptr, d->has_perlin ? sizeof(double) * 768 : 0, 0},
+        {d->has_perlin ? d->perlin_perm : nullptr, d->has_perlin ? sizeof(int32_t) * 768 : 0, 0},
+        {media.data(), sizeof(int32_t) * media.size(), 0},
+    };
+    size_t total = 0;
+    for (auto& p : parts) {
+        p.off = total;
+        total += (p.bytes + 255) & ~size_t(255);
+    }
+    int rc = h->scene_mem.ensure(std::max<size_t>(total, 256));
+    if (rc) return rc;
+    std::vector<char> staging(std::max<size_t>(total, 256), 0);
+    for (auto& p : parts)
+        if (p.bytes && p.src) std::memcpy(staging.data() + p.off, p.src, p.bytes);
+    HIPCHK(hipMemcpy(h->scene_mem.p, staging.data(), staging.size(), hipMemcpyHostToDevice));
+    char* base = static_cast<char*>(h->scene_mem.p);
+    auto at = [&](int k) { return parts[k].bytes ? (void*)(base + parts[k].off) : nullptr; };
+    scene& S = h->S;
+    S.prims = (const rtw_prim*)at(0);
+    S.entries = (const rtw_entry*)at(1);
+    S.materials = (const rtw_material*)at(2);
+    S.textures = (const rtw_texture*)at(3);
+    S.lights = (const rtw_light*)at(4);
+    S.nodes = (const rtw_bvh_node*)at(5);
+    S.items = (const int32_t*)at(6);
+    S.ranvec = (const double*)at(7);
+    S.perm = (const int32_t*)at(8);
+    S.media = (const int32_t*)at(9);
+    S.n_entries = d->n_entries;
+    S.n_lights = d->n_lights;
+    S.world_bvh_root = d->world_bvh_root;
+    S.render_type = d->render_type;
+    S.background = d->background;
+    S.n_media = (int32_t)media.size();
+    S.has_media = media.empty() ? 0 : 1;
+    h->media = !media.empty();
+    return RTW_OK;
+}
+
+int validate_desc(const rtw_scene_desc* d) {
+    if (!d) return rtw_fail(RTW_ERR_INVALID, "null scene desc");
+    if (d->abi_version != RTW_ABI_VERSION) return rtw_fail(RTW_ERR_INVALID, "scene desc ABI version mismatch");
+    if (d->n_entries < 0 || d->n_prims < 0 || d->n_materials < 0 || d->n_textures < 0 || d->n_lights < 0)
+        return rtw_fail(RTW_ERR_INVALID, "negative array size in scene desc");
+    for (int e = 0; e < d->n_entries; ++e) {
+        const rtw_entry& E = d->entries[e];
+        if (E.first_prim < 0 || E.n_prims <= 0 || E.first_prim + E.n_prims > d->n_prims)
+            return rtw_fail(RTW_ERR_INVALID, "entry " + std::to_string(e) + ": prim range out of bounds");
+        if (E.n_ops < 0 || E.n_ops > RTW_MAX_OPS) return rtw_fail(RTW_ERR_INVALID, "entry op count out of range");
+        if (E.kind == RTW_ENTRY_MEDIUM && (E.phase_material < 0 || E.phase_material >= d->n_materials))
+            return rtw_fail(RTW_ERR_INVALID, "medium phase material out of range");
+        if (E.bvh_root >= d->n_bvh_nodes) return rtw_fail(RTW_ERR_INVALID, "entry bvh root out of range");
+        if (E.kind == RTW_ENTRY_MEDIUM && d->world_bvh_root >= 0)
+            return rtw_fail(RTW_ERR_UNSUPPORTED, "a world BVH cannot hold media (list order matters for their draws)");
+    }
+    for (int p = 0; p < d->n_prims; ++p) {
+        const rtw_prim& P = d->prims[p];
+        if (P.type < RTW_PRIM_SPHERE || P.type > RTW_PRIM_RECT_YZ) return rtw_fail(RTW_ERR_INVALID, "bad prim type");
+        if (P.material < 0 || P.material >= d->n_materials) return rtw_fail(RTW_ERR_INVALID, "prim material out of range");
+        if (P.entry >= d->n_entries) return rtw_fail(RTW_ERR_INVALID, "prim entry out of range");
+    }
+    for (int m = 0; m < d->n_materials; ++m) {
+        const rtw_material& M = d->materials[m];
+        const bool tex = M.type == RTW_MAT_LAMBERTIAN || M.type == RTW_MAT_DIFFUSE_LIGHT || M.type == RTW_MAT_ISOTROPIC;
+        if (M.type < RTW_MAT_LAMBERTIAN || M.type > RTW_MAT_ISOTROPIC) return rtw_fail(RTW_ERR_INVALID, "bad material type");
+        if (tex && (M.texture < 0 || M.texture >= d->n_textures)) return rtw_fail(RTW_ERR_INVALID, "material texture out of range");
+    }
+    for (int t = 0; t < d->n_textures; ++t) {
+        const rtw_texture& T = d->textures[t];
+        if (T.type == RTW_TEX_NOISE && !d->has_perlin) return rtw_fail(RTW_ERR_INVALID, "noise texture without perlin tables");
+        if (T.type == RTW_TEX_CHECKER && (T.odd < 0 || T.odd >= d->n_textures || T.even < 0 || T.even >= d->n_textures))
+            return rtw_fail(RTW_ERR_INVALID, "checker child out of range");
+    }
+    for (int l = 0; l < d->n_lights; ++l) {
+        const rtw_light& L = d->lights[l];
+        if (L.kind != RTW_LIGHT_DEFAULT && (L.prim < 0 || L.prim >= d->n_prims))
+            return rtw_fail(RTW_ERR_INVALID, "light prim out of range");
+    }
+    if (d->world_bvh_root >= d->n_bvh_nodes) return rtw_fail(RTW_ERR_INVALID, "world bvh root out of range");
+    for (int k = 0; k < d->n_bvh_nodes; ++k) {
+        const rtw_bvh_node& N = d->bvh_nodes[k];
+        if (N.count > 0 ? (N.left < 0 || N.left + N.count > d->n_bvh_items)
+                        : (N.left < 0 || N.left >= d->n_bvh_nodes || N.right < 0 || N.right >= d->n_bvh_nodes))
+            return rtw_fail(RTW_ERR_INVALID, "bvh node out of range");
+    }
+    return RTW_OK;
+}
+
+hipEvent_t event_at(handle_t* h, size_t k) {
+    while (h->events.size() <= k) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        h->events.push_back(e);
+    }
+    return h->events[k];
+}
+
+size_t pass_budget_samples() {
+    if (const char* s = std::getenv("RTW_PASS_SAMPLES")) {
+        const long long v = std::atoll(s);
+        if (v > 0) return (size_t)v;
+    }
+    return size_t(1) << 28;  // 6 GiB of fp64 radiance planes per pass
+}
+
+}  // namespace
+
+extern "C" int rtw_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" int rtw_scene_upload(int device, const rtw_scene_desc* desc, void** out_handle) {
+    if (!out_handle) return rtw_fail(RTW_ERR_INVALID, "rtw_scene_upload: null out_handle");
+    *out_handle = nullptr;
+    int rc = validate_desc(desc);
+    if (rc) return rc;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return rtw_fail(RTW_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return rtw_fail(RTW_ERR_INVALID, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return rtw_fail(RTW_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+    handle_t* h = new handle_t;
+    h->device = device;
+    h->grid = prop.multiProcessorCount * 8;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return rtw_fail(RTW_ERR_HIP, "hipStreamCreate failed");
+    }
+    rc = upload_scene(h, desc);
+    if (!rc) rc = h->ctrs.ensure(sizeof(ctrs_t));
+    if (!rc && hipHostMalloc((void**)&h->host_ctrs, sizeof(ctrs_t) * 64, hipHostMallocDefault) != hipSuccess)
+        rc = rtw_fail(RTW_ERR_OOM, "hipHostMalloc failed");
+    if (rc) {
+        rtw_scene_free(h);
+        return rc;
+    }
+    *out_handle = h;
+    return RTW_OK;
+}
+
+extern "C" void rtw_scene_free(void* handle) {
+    handle_t* h = static_cast<handle_t*>(handle);
+    if (!h) return;
+    hipSetDevice(h->device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    h->scene_mem.release();
+    h->pool[0].release();
+    h->pool[1].release();
+    h->hits.release();
+    h->radiance.release();
+    h->run.release();
+    h->accum.release();
+    h->ctrs.release();
+    if (h->host_ctrs) hipHostFree(h->host_ctrs);
+    for (hipEvent_t e : h->events) hipEventDestroy(e);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+}
+
+extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera, const rtw_render_params* prm,
+                                     double* accum_rgb, rtw_stats* out_stats) {
+    handle_t* h = static_cast<handle_t*>(handle);
+    if (!h || !camera || !prm || !accum_rgb) return rtw_fail(RTW_ERR_INVALID, "rtw_render_accumulate: null argument");
+    const rtw_render_params& R = *prm;
+    if (R.nx <= 0 || R.ny <= 0 || R.spp <= 0 || R.spp_begin < 0 || R.spp_begin > R.spp || R.spp_count < 0)
+        return rtw_fail(RTW_ERR_INVALID, "rtw_render_accumulate: bad image / sample parameters");
+    const int spp_count = R.spp_count ? R.spp_count : R.spp - R.spp_begin;
+    if (R.spp_begin + (long long)spp_count > R.spp) return rtw_fail(RTW_ERR_INVALID, "sample range exceeds spp");
+    const int row_step = R.row_step > 0 ? R.row_step : 1;
+    if (R.row_begin < 0 || R.row_begin >= R.ny) return rtw_fail(RTW_ERR_INVALID, "row_begin out of range");
+    const int n_rows = (R.ny - R.row_begin + row_step - 1) / row_step;
+    const uint64_t npix = (uint64_t)n_rows * (uint64_t)R.nx;
+    if ((uint64_t)R.nx * R.ny >= (1ull << 32) || npix >= (1ull << 31))
+        return rtw_fail(RTW_ERR_INVALID, "image too large for 32-bit pixel ids");
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t st = h->stream;
+
+    rtw_stats stats;
+    std::memset(&stats, 0, sizeof stats);
+    if (spp_count == 0 || R.max_depth <= 0) {
+        // color() with depth <= 0 returns 0 (RayTracingWeekend.cpp:47-48):
+        // every sample adds zero radiance, the accumulator is unchanged.
+        stats.samples = (uint64_t)spp_count * npix;
+        if (out_stats) *out_stats = stats;
+        return RTW_OK;
+    }
+
+    // pool and pass sizing
+    uint32_t pool = R.wavefront_paths > 0 ? (uint32_t)R.wavefront_paths : (1u << 21);
+    const size_t budget = pass_budget_samples();
+    uint64_t pass_spp = std::max<uint64_t>(1, std::min<uint64_t>(spp_count, budget / npix));
+    pass_spp = std::min<uint64_t>(pass_spp, ((1ull << 32) - 1) / npix);
+    const uint64_t pass_samples = pass_spp * npix;
+    pool = (uint32_t)std::min<uint64_t>(pool, pass_samples);
+    pool = std::max<uint32_t>(pool, 1);
+
+    int rc;
+    if ((rc = h->pool[0].ensure(paths_bytes(pool)))) return rc;
+    if ((rc = h->pool[1].ensure(paths_bytes(pool)))) return rc;
+    if ((rc = h->hits.ensure((size_t)pool * 12))) return rc;
+    if ((rc = h->radiance.ensure(pass_samples * 24))) return rc;
+    if ((rc = h->run.ensure(npix * 24))) return rc;
+    paths_t A = carve_paths(h->pool[0].p, pool), B = carve_paths(h->pool[1].p, pool);
+    double* ht = static_cast<double*>(h->hits.p);
+    int32_t* hid = reinterpret_cast<int32_t*>(static_cast<char*>(h->hits.p) + (size_t)pool * 8);
+    ctrs_t* C = static_cast<ctrs_t*>(h->ctrs.p);
+    double* run = static_cast<double*>(h->run.p);
+    HIPCHK(hipMemsetAsync(run, 0, npix * 24, st));
+    HIPCHK(hipMemsetAsync(C, 0, sizeof(ctrs_t), st));
+
+    job_t J;
+    J.cam = *camera;
+    J.seed_mix = host_splitmix64(R.seed);
+    J.npix = (uint32_t)npix;
+    J.nx = R.nx, J.ny = R.ny, J.row_begin = R.row_begin, J.row_step = row_step;
+    J.max_depth = R.max_depth;
+    J.Lr = static_cast<double*>(h->radiance.p);
+    J.Lg = J.Lr + pass_samples;
+    J.Lb = J.Lg + pass_samples;
+
+    const int grid = h->grid;
+    size_t ev = 0;
+    std::vector<std::pair<size_t, size_t>> isect_ev, shade_ev;
+    hipEvent_t ev_begin = event_at(h, ev++), ev_end = event_at(h, ev++);
+    if (!ev_begin || !ev_end) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
+    HIPCHK(hipEventRecord(ev_begin, st));
+    const bool timed = R.collect_kernel_times != 0;
+    const int check_every = 4;
+
+    for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
+        const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
+        J.total = (uint32_t)(S_pass * npix);
+        J.s_begin = R.spp_begin + (int)done;
+        const uint32_t n0 = std::min<uint32_t>(pool, J.total);
+        hipLaunchKernelGGL(k_fill, dim3((n0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, J, A, C, n0);
+        HIPCHK(hipGetLastError());
+        bool tail = false;
+        std::vector<size_t> checks;  // event slots of status copies, with their copy index
+        for (uint64_t it = 0;; ++it) {
+            {
+                size_t e0 = 0, e1 = 0;
+                if (timed) {
+                    e0 = ev++, e1 = ev++;
+                    if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
+                    HIPCHK(hipEventRecord(h->events[e0], st));
+                }
+                if (h->media)
+                    hipLaunchKernelGGL(k_intersect<true>, dim3(grid), dim3(kBlock), 0, st, h->S, A, ht, hid, C);
+                else
+                    hipLaunchKernelGGL(k_intersect<false>, dim3(grid), dim3(kBlock), 0, st, h->S, A, ht, hid, C);
+                if (timed) {
+                    HIPCHK(hipEventRecord(h->events[e1], st));
+                    isect_ev.push_back({e0, e1});
+                    e0 = ev++, e1 = ev++;
+                    if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
+                    HIPCHK(hipEventRecord(h->events[e0], st));
+                }
+                hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kBlock), 0, st, h->S, J, A, ht, hid, C);
+                if (timed) {
+                    HIPCHK(hipEventRecord(h->events[e1], st));
+                    shade_ev.push_back({e0, e1});
+                }
+                HIPCHK(hipGetLastError());
+                stats.launches_intersect++;
+                stats.iterations++;
+                if (tail) {
+                    hipLaunchKernelGGL(k_compact, dim3(grid), dim3(kBlock), 0, st, A, B, C);
+                    hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, st, C);
+                    HIPCHK(hipGetLastError());
+                    std::swap(A, B);
+                }
+            }
+            if (it % check_every == check_every - 1) {
+                // status snapshot; decide from the previous snapshot so the GPU
+                // keeps `check_every` iterations of queued work
+                const size_t slot = checks.size() % 64;
+                HIPCHK(hipMemcpyAsync(&h->host_ctrs[slot], C, sizeof(ctrs_t), hipMemcpyDeviceToHost, st));
+                const size_t e = ev++;
+                if (!event_at(h, e)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
+                HIPCHK(hipEventRecord(h->events[e], st));
+                checks.push_back(e);
+                const size_t idx = checks.size() >= 2 ? checks.size() - 2 : 0;
+                HIPCHK(hipEventSynchronize(h->events[checks[idx]]));
+                const ctrs_t snap = h->host_ctrs[idx % 64];
+                if (snap.q_next >= J.total) tail = true;
+                if (tail && snap.n == 0) break;
+            }
+        }
+        hipLaunchKernelGGL(k_reduce, dim3(std::min<uint64_t>((npix + kBlock - 1) / kBlock, 4096)), dim3(kBlock), 0, st,
+                           J.Lr, J.Lg, J.Lb, (uint32_t)npix, S_pass, run);
+        HIPCHK(hipGetLastError());
+        stats.samples += J.total;
+    }
+
+    // accum += run
+    double* acc_dev = accum_rgb;
+    const size_t img_bytes = (size_t)R.nx * R.ny * 24;
+    if (!R.accum_on_device) {
+        if ((rc = h->accum.ensure(img_bytes))) return rc;
+        acc_dev = static_cast<double*>(h->accum.p);
+        HIPCHK(hipMemcpyAsync(acc_dev, accum_rgb, img_bytes, hipMemcpyHostToDevice, st));
+    }
+    hipLaunchKernelGGL(k_emit, dim3(std::min<uint64_t>((npix + kBlock - 1) / kBlock, 4096)), dim3(kBlock), 0, st, run,
+                       (uint32_t)npix, R.nx, R.row_begin, row_step, acc_dev);
+    HIPCHK(hipGetLastError());
+    if (!R.accum_on_device) HIPCHK(hipMemcpyAsync(accum_rgb, acc_dev, img_bytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&h->host_ctrs[63], C, sizeof(ctrs_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(ev_end, st));
+    HIPCHK(hipStreamSynchronize(st));
+
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, ev_begin, ev_end));
+    stats.ms_total = ms;
+    stats.segments = h->host_ctrs[63].segments;
+    for (auto& p : isect_ev) {
+        HIPCHK(hipEventElapsedTime(&ms, h->events[p.first], h->events[p.second]));
+        stats.ms_intersect += ms;
+    }
+    for (auto& p : shade_ev) {
+        HIPCHK(hipEventElapsedTime(&ms, h->events[p.first], h->events[p.second]));
+        stats.ms_shade += ms;
+    }
+    stats.bytes_intersect = 68.0 * (double)stats.segments;  // 56 B ray in + 12 B hit out
+    if (out_stats) *out_stats = stats;
+    return RTW_OK;
+}

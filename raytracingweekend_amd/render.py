@@ -1,0 +1,137 @@
+"""Host-side Python API over the C ABI: the render loop of
+RayTracingWeekend.cpp:195-289 (scene -> canvas -> PPM) with the per-pixel work
+on the GPU.
+
+    from raytracingweekend_amd import render
+    canvas, stats = render.render("cornell_box", 400, 400, spp=64, max_depth=100)
+    render.write_ppm("x64/1.ppm", canvas, 400, 400)
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL): see
+raytracingweekend_amd.distributed.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _abi
+from ._abi import check, lib
+
+
+class SceneDesc:
+    """A reference scene built with the host C++ scene API and flattened
+    (rtw_scene_builtin).  Owns the library-allocated rtw_scene_desc."""
+
+    def __init__(self, name: str, aspect: float, use_bvh: bool = False):
+        self.name = name
+        self.aspect = float(aspect)
+        self.use_bvh = bool(use_bvh)
+        p = C.POINTER(_abi.rtw_scene_desc)()
+        check(lib().rtw_scene_builtin(name.encode(), self.aspect, int(use_bvh), C.byref(p)), "rtw_scene_builtin")
+        self.ptr = p
+
+    @property
+    def desc(self) -> _abi.rtw_scene_desc:
+        return self.ptr.contents
+
+    @property
+    def camera(self) -> _abi.rtw_camera_desc:
+        return self.ptr.contents.camera
+
+    def close(self):
+        if self.ptr:
+            lib().rtw_scene_desc_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceScene:
+    """A scene uploaded to one GPU (rtw_scene_upload)."""
+
+    def __init__(self, scene: SceneDesc, device: int = 0):
+        self.scene = scene
+        self.device = device
+        h = C.c_void_p()
+        check(lib().rtw_scene_upload(device, scene.ptr, C.byref(h)), "rtw_scene_upload")
+        self.handle = h
+
+    def render_accumulate(self, nx: int, ny: int, spp: int, max_depth: int, seed: int = 0, *,
+                          spp_begin: int = 0, spp_count: int = 0, row_begin: int = 0, row_step: int = 1,
+                          accum=None, camera: Optional[_abi.rtw_camera_desc] = None,
+                          collect_kernel_times: bool = False, wavefront_paths: int = 0):
+        """Add the per-pixel radiance sums of the selected samples into `accum`
+        (a float64 numpy array of nx*ny*3, or a torch float64 CUDA tensor on
+        this device).  Returns (accum, stats dict)."""
+        if accum is None:
+            accum = np.zeros(nx * ny * 3, dtype=np.float64)
+        on_device = 0
+        if isinstance(accum, np.ndarray):
+            if accum.dtype != np.float64 or accum.size != nx * ny * 3 or not accum.flags["C_CONTIGUOUS"]:
+                raise ValueError("accum must be a contiguous float64 array of nx*ny*3")
+            ptr = accum.ctypes.data_as(C.c_void_p)
+        else:  # torch tensor on the device
+            import torch
+            if accum.dtype != torch.float64 or accum.numel() != nx * ny * 3 or not accum.is_contiguous():
+                raise ValueError("accum must be a contiguous float64 tensor of nx*ny*3")
+            if not accum.is_cuda:
+                raise ValueError("a torch accum must live on the GPU")
+            torch.cuda.synchronize(accum.device)
+            ptr = C.c_void_p(accum.data_ptr())
+            on_device = 1
+        prm = _abi.rtw_render_params(nx=nx, ny=ny, spp=spp, max_depth=max_depth, seed=seed, spp_begin=spp_begin,
+                                     spp_count=spp_count, row_begin=row_begin, row_step=row_step,
+                                     accum_on_device=on_device, collect_kernel_times=int(collect_kernel_times),
+                                     wavefront_paths=wavefront_paths, reserved=0)
+        st = _abi.rtw_stats()
+        cam = camera if camera is not None else self.scene.camera
+        check(lib().rtw_render_accumulate(self.handle, C.byref(cam), C.byref(prm), ptr, C.byref(st)),
+              "rtw_render_accumulate")
+        return accum, st.as_dict()
+
+    def close(self):
+        if self.handle:
+            lib().rtw_scene_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    return lib().rtw_device_count()
+
+
+def finalize(accum: np.ndarray, nx: int, ny: int, spp: int) -> np.ndarray:
+    """canvas = min(sqrt(sum / spp), 1) (RayTracingWeekend.cpp:241-244), via the
+    library's rtw_finalize_canvas."""
+    a = np.ascontiguousarray(accum, dtype=np.float64)
+    out = np.empty(nx * ny * 3, dtype=np.float64)
+    lib().rtw_finalize_canvas(a.ctypes.data_as(C.c_void_p), nx, ny, spp, out.ctypes.data_as(C.c_void_p))
+    return out
+
+
+def write_ppm(path: str, canvas: np.ndarray, nx: int, ny: int) -> None:
+    c = np.ascontiguousarray(canvas, dtype=np.float64)
+    check(lib().rtw_write_ppm(str(path).encode(), c.ctypes.data_as(C.c_void_p), nx, ny), "rtw_write_ppm")
+
+
+def render(scene: str, nx: int, ny: int, spp: int, max_depth: int, seed: int = 0, device: int = 0,
+           use_bvh: bool = False, **kw) -> Tuple[np.ndarray, dict]:
+    """Render `scene` at nx*ny*spp on one GPU; returns (canvas, stats)."""
+    sd = SceneDesc(scene, nx * 1.0 / ny, use_bvh)
+    ds = DeviceScene(sd, device)
+    try:
+        accum, stats = ds.render_accumulate(nx, ny, spp, max_depth, seed, **kw)
+    finally:
+        ds.close()
+    return finalize(accum, nx, ny, spp), stats

@@ -1,0 +1,83 @@
+"""Loader for the test-only oracle (oracle/_ref/librtw_oracle.so, the plain-C
+restatement of the reference).  Tests, smoke() and bench.py's cpu_baseline are
+the only users."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+ORACLE_SO = ROOT / "oracle" / "_ref" / "librtw_oracle.so"
+REF_BIN = ROOT / "oracle" / "_ref" / "rtw_ref"
+
+_lib = None
+
+
+def oracle():
+    global _lib
+    if _lib is None:
+        if not ORACLE_SO.exists():
+            subprocess.run(["make", "-C", str(ROOT / "oracle"), "port"], check=True, capture_output=True)
+        from raytracingweekend_amd import _abi
+        L = C.CDLL(str(ORACLE_SO))
+        L.rtw_oracle_render.restype = C.c_int
+        L.rtw_oracle_render.argtypes = [C.POINTER(_abi.rtw_scene_desc), C.POINTER(_abi.rtw_camera_desc), C.c_int,
+                                        C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int,
+                                        C.c_void_p, C.POINTER(C.c_uint64)]
+        L.rtw_oracle_trace.restype = C.c_int
+        L.rtw_oracle_trace.argtypes = [C.POINTER(_abi.rtw_scene_desc), C.POINTER(_abi.rtw_camera_desc), C.c_int,
+                                       C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
+                                       C.c_void_p, C.c_int]
+        L.rtw_oracle_canonical.restype = C.c_double
+        L.rtw_oracle_canonical.argtypes = [C.POINTER(C.c_uint32)]
+        L.rtw_oracle_noise.restype = C.c_double
+        L.rtw_oracle_noise.argtypes = [C.POINTER(_abi.rtw_scene_desc), C.POINTER(C.c_double * 3)]
+        L.rtw_oracle_turb.restype = C.c_double
+        L.rtw_oracle_turb.argtypes = [C.POINTER(_abi.rtw_scene_desc), C.POINTER(C.c_double * 3)]
+        L.rtw_oracle_path_seed.restype = C.c_uint32
+        L.rtw_oracle_path_seed.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
+        _lib = L
+    return _lib
+
+
+def oracle_sums(scene_desc, nx, ny, spp, max_depth, seed=0, threads=0, rows=None, spp_begin=0, spp_count=None,
+                camera=None):
+    """Per-pixel radiance sums (nx*ny*3 float64) from the C restatement."""
+    out = np.zeros(nx * ny * 3, dtype=np.float64)
+    seg = C.c_uint64(0)
+    r0, rc = (0, ny) if rows is None else rows
+    cnt = spp if spp_count is None else spp_count
+    cam = camera if camera is not None else scene_desc.camera
+    rcode = oracle().rtw_oracle_render(scene_desc.ptr, C.byref(cam), nx, ny, r0, rc, spp_begin, cnt, max_depth,
+                                       seed, threads, out.ctypes.data_as(C.c_void_p), C.byref(seg))
+    assert rcode == 0
+    return out, seg.value
+
+
+def ref_available() -> bool:
+    return REF_BIN.exists()
+
+
+def ref_sums(scene: str, nx, ny, spp, max_depth, seed=0, threads=8):
+    """Per-pixel sums from the reference's own code (oracle/_ref/rtw_ref)."""
+    import json
+    import tempfile
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        path = f.name
+    try:
+        r = subprocess.run([str(REF_BIN), "render", scene, str(nx), str(ny), str(spp), str(max_depth), str(seed),
+                            str(threads), path], check=True, capture_output=True, text=True)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        return np.fromfile(path, dtype=np.float64), info
+    finally:
+        os.unlink(path)
+
+
+def finalize_np(sums, spp):
+    """RayTracingWeekend.cpp:241-244 in numpy (same IEEE ops)."""
+    s = np.sqrt(sums / float(spp))
+    return np.where(1.0 < s, 1.0, s)
