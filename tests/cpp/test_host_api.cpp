@@ -1,0 +1,106 @@
+// Host scene API checks, compiled and run by tests/test_host_api.py.
+//  * the reference's own unit-test assertions (CppTest/unittest1.cpp:20-109:
+//    dot, cross, ray::point_at_parameter, aabb::hit, aabb::surrounding);
+//  * scene code written against the reference's API (Scene/scene.h style)
+//    compiles unchanged against these headers and flattens.
+#include <cfloat>
+#include <cstdio>
+#include <memory>
+#include "rtw/scene.h"
+
+static int failures = 0;
+#define CHECK(c)                                                   \
+    do {                                                           \
+        if (!(c)) {                                                \
+            std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c); \
+            ++failures;                                            \
+        }                                                          \
+    } while (0)
+
+// A user scene in the reference's idiom: derive from scene, Add() objects,
+// push lights, set cam/background (Scene/scene.h:176-250 style).
+class user_scene : public scene {
+public:
+    user_scene(double aspect) : scene() {
+        std::shared_ptr<texture> red_tex = std::make_shared<constant_texture>(vec3(0.65f, 0.05f, 0.05f));
+        auto red = std::make_shared<lambertian>(red_tex);
+        auto light = std::make_shared<diffuse_light>(std::make_shared<constant_texture>(vec3(15.0, 15.0, 15.0)));
+        std::shared_ptr<texture> t0 = std::make_shared<constant_texture>(vec3(0.2, 0.3, 0.1));
+        std::shared_ptr<texture> t1 = std::make_shared<constant_texture>(vec3(0.9, 0.9, 0.9));
+        auto checker = std::make_shared<lambertian>(std::make_shared<checker_texture>(t0, t1));
+        auto lamp = std::make_shared<xz_rect>(213.0, 343.0, 227.0, 332.0, 554.0, light);
+        Add(lamp);
+        lights->objects.push_back(lamp);
+        Add(std::make_shared<flip_normals>(std::make_shared<yz_rect>(0.0, 555.0, 0.0, 555.0, 555.0, red)));
+        Add(std::make_shared<sphere>(vec3(190, 90, 190), 90, checker));
+        Add(std::make_shared<translate>(
+            std::make_shared<rotate_y>(std::make_shared<box>(vec3(0, 0, 0), vec3(165, 330, 165), red), 15.0),
+            vec3(265, 0, 295)));
+        Add(std::make_shared<constant_medium>(
+            std::make_shared<box>(vec3(0, 0, 0), vec3(10, 10, 10), red), 0.01,
+            std::make_shared<isotropic>(std::make_shared<constant_texture>(vec3(1, 1, 1)))));
+        moving_sphere* ms = new moving_sphere(vec3(1, 2, 3), 1.0, red);
+        movement_linear m;
+        m.center1 = vec3(1, 3, 3);
+        ms->set_movement(m);
+        Add(std::shared_ptr<hittable>(ms));
+        cam = camera(vec3(278.0, 278.0, -800.0), vec3(278.0, 278.0, 0.0), vec3(0.0, 1.0, 0.0), 40.0, aspect, 0.0,
+                     10.0, 0.0, 1.0);
+        background_type = BackgroundType::Black;
+    }
+};
+
+int main() {
+    // CppTest/unittest1.cpp:20-40
+    CHECK(dot(vec3(1, 1, 0), vec3(1, 1, 0)) == 2.0);
+    vec3 c = cross(vec3(1, 0, 0), vec3(0, 1, 0));
+    CHECK(c.x == 0.0 && c.y == 0.0 && c.z == 1.0);
+    ray r(vec3(1, 1, 1), vec3(2, 2, 2), 0.0);
+    CHECK(r.point_at_parameter(3).x == 7.0 && r.point_at_parameter(3).y == 7.0 && r.point_at_parameter(3).z == 7.0);
+    // CppTest/unittest1.cpp:72-93 (axis-parallel rays: 1/0 = +-inf slabs)
+    aabb b(vec3(2, 2, 2), vec3(4, 4, 4));
+    CHECK(b.hit(ray(vec3(0, 0, 0), vec3(1, 1, 1), 0.0), 0, FLT_MAX));
+    CHECK(!b.hit(ray(vec3(0, 0, 0), -vec3(1, 1, 1), 0.0), 0, FLT_MAX));
+    CHECK(b.hit(ray(vec3(3, 3, 3), vec3(0, 1, 0), 0.0), 0, FLT_MAX));
+    CHECK(b.hit(ray(vec3(0, 3, 0), vec3(1, 0, 1), 0.0), 0, FLT_MAX));
+    CHECK(!b.hit(ray(vec3(0, 5, 0), vec3(1, 0, 1), 0.0), 0, FLT_MAX));
+    // CppTest/unittest1.cpp:95-109
+    aabb b0(vec3(0, 0, 0), vec3(1, 1, 1)), b1(vec3(3, 3, 3), vec3(4, 4, 4));
+    aabb s = aabb::surrounding(b0, b1);
+    CHECK(s.min()[0] == 0.0 && s.min()[1] == 0.0 && s.min()[2] == 0.0);
+    CHECK(s.max()[0] == 4.0 && s.max()[1] == 4.0 && s.max()[2] == 4.0);
+    // vec3 aliases (vec3.h:35-44)
+    vec3 col;
+    col.r = 0.25;
+    CHECK(col.x == 0.25 && col.e[0] == 0.25);
+
+    user_scene us(1.0);
+    rtw_scene_desc* d = nullptr;
+    CHECK(rtw_flatten_scene(us, 0, &d) == RTW_OK);
+    if (d) {
+        CHECK(d->n_entries == 6);
+        CHECK(d->entries[3].n_ops == 2 && d->entries[3].n_prims == 6);
+        CHECK(d->entries[4].kind == RTW_ENTRY_MEDIUM && d->entries[4].n_prims == 6);
+        CHECK(d->n_lights == 1 && d->lights[0].kind == RTW_LIGHT_XZ_RECT);
+        CHECK(d->prims[1].flip == 1);
+        CHECK(d->prims[d->entries[5].first_prim].type == RTW_PRIM_MOVING_SPHERE);
+        int checkers = 0;
+        for (int t = 0; t < d->n_textures; ++t) checkers += d->textures[t].type == RTW_TEX_CHECKER;
+        CHECK(checkers == 1);
+        rtw_scene_desc_free(d);
+    }
+    // the BVH-backed bvh_node container flattens as a group
+    std::vector<std::shared_ptr<hittable>> balls;
+    auto mat = std::make_shared<metal>(vec3(0.5, 0.5, 0.5), 0.1);
+    for (int k = 0; k < 20; ++k) balls.push_back(std::make_shared<sphere>(vec3(k, 0, 0), 0.4, mat));
+    scene sc;
+    sc.Add(std::make_shared<bvh_node>(balls, 0.0, 1.0));
+    rtw_scene_desc* d2 = nullptr;
+    CHECK(rtw_flatten_scene(sc, 1, &d2) == RTW_OK);
+    if (d2) {
+        CHECK(d2->n_entries == 1 && d2->entries[0].n_prims == 20 && d2->entries[0].bvh_root >= 0);
+        rtw_scene_desc_free(d2);
+    }
+    std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
+    return failures ? 1 : 0;
+}

@@ -1,0 +1,88 @@
+"""N > 1 path on CPU: world_size-2 gloo ranks run render_sharded with the
+oracle standing in for each rank's GPU renderer (test-only injection), and the
+reduced canvas on rank 0 equals the single-process render."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from raytracingweekend_amd.distributed import render_sharded, sample_range
+
+NX, NY, SPP, DEPTH, SEED = 20, 16, 5, 50, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_fn(sd):
+    from oracle_lib import oracle_sums
+
+    def fn(spp_begin, spp_count, row_begin, row_step, accum):
+        rows = list(range(row_begin, NY, row_step))
+        out = np.zeros(NX * NY * 3)
+        for j in rows:
+            s, _ = oracle_sums(sd, NX, NY, SPP, DEPTH, SEED, threads=1, rows=(j, 1), spp_begin=spp_begin,
+                               spp_count=spp_count)
+            out += s
+        accum += torch.from_numpy(out)
+
+    return fn
+
+
+def _worker(rank, world, port, mode, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(root))
+    sys.path.insert(0, str(root / "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from raytracingweekend_amd.render import SceneDesc
+    sd = SceneDesc("cornell_box", NX / NY)
+    accum = torch.zeros(NX * NY * 3, dtype=torch.float64)
+    canvas = render_sharded(_oracle_fn(sd), NX, NY, SPP, accum, mode=mode)
+    if rank == 0:
+        q.put(canvas)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["spp", "rows"])
+def test_two_rank_gloo_matches_single(built, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    canvas = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    from oracle_lib import finalize_np, oracle_sums
+    from raytracingweekend_amd.render import SceneDesc
+    full, _ = oracle_sums(SceneDesc("cornell_box", NX / NY), NX, NY, SPP, DEPTH, SEED)
+    want = finalize_np(full, SPP)
+    if mode == "rows":
+        assert np.array_equal(canvas, want)
+    else:
+        assert np.allclose(canvas, want, rtol=1e-13, atol=1e-13)
+
+
+def test_sample_range_partition():
+    for spp in (1, 7, 64, 1024):
+        for world in (1, 2, 3, 8):
+            got = [sample_range(spp, world, r) for r in range(world)]
+            assert sum(c for _, c in got) == spp
+            pos = 0
+            for b, c in got:
+                assert b == pos
+                pos += c
