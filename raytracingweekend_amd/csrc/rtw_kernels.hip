@@ -40,13 +40,30 @@ struct paths_t {
     uint32_t *rng, *depth, *qid;
 };
 
+// The sample queue is sharded over kQShards counters to spread the atomics:
+// shard s owns the chunks c = s, s + kQShards, ... of kQChunk consecutive
+// samples, and its j-th sample is  q = ((j / kQChunk) * kQShards + s) * kQChunk
+// + j % kQChunk.
+constexpr int kQShards = 8;
+constexpr uint32_t kQChunk = 1024;
+
 struct ctrs_t {
-    unsigned long long q_next;   // next sample index of the pass to hand out
-    unsigned long long segments; // world hit queries (live paths intersected)
-    unsigned int n;              // slots in the current pool
-    unsigned int n_out;          // compaction output count
+    unsigned long long qshard[kQShards]; // per-shard count of samples handed out
+    unsigned long long segments;         // world hit queries (live paths intersected)
+    unsigned int n;                      // slots in the current pool
+    unsigned int n_out;                  // compaction output count
     unsigned int pad[4];
 };
+
+__host__ __device__ inline uint64_t shard_sample(int s, uint64_t j) {
+    return ((j / kQChunk) * kQShards + (uint64_t)s) * kQChunk + j % kQChunk;
+}
+// number of the pass's `total` samples that shard s owns (its ids 0..limit-1)
+__host__ __device__ inline uint64_t shard_limit(int s, uint64_t total) {
+    const uint64_t full = total / kQChunk, rem = total % kQChunk;
+    const uint64_t nfull = full > (uint64_t)s ? (full - (uint64_t)s + kQShards - 1) / kQShards : 0;
+    return nfull * kQChunk + ((full % kQShards) == (uint64_t)s ? rem : 0);
+}
 
 struct job_t {
     rtw_camera_desc cam;
@@ -85,13 +102,12 @@ __device__ __forceinline__ void raygen(const job_t& J, const paths_t& P, uint32_
     P.qid[slot] = q;
 }
 
-__global__ __launch_bounds__(kBlock) void k_fill(job_t J, paths_t P, ctrs_t* C, uint32_t n0) {
+// Start a pass: slots [0, n0) empty (depth 0) for k_regen to fill.
+__global__ __launch_bounds__(kBlock) void k_fill(paths_t P, ctrs_t* C, uint32_t n0) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i < n0) raygen(J, P, i, i);
-    if (i == 0) {
-        C->n = n0;
-        C->q_next = n0;
-    }
+    if (i < n0) P.depth[i] = 0;
+    if (i == 0) C->n = n0;
+    if (i < kQShards) C->qshard[i] = 0;
 }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() {
@@ -117,7 +133,7 @@ __device__ __forceinline__ uint32_t block_rank(bool flag, uint32_t* s_wave, uint
     return before + (uint32_t)__popcll(m & lanemask_lt());
 }
 
-template <bool MEDIA>
+template <int F>
 __global__ __launch_bounds__(kBlock) void k_intersect(scene S, paths_t P, double* __restrict__ ht,
                                                       int32_t* __restrict__ hid, ctrs_t* C) {
     __shared__ uint32_t s_cnt[kWaves];
@@ -126,9 +142,9 @@ __global__ __launch_bounds__(kBlock) void k_intersect(scene S, paths_t P, double
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         if (P.depth[i] == 0) continue;
         const ray r{d3{P.ox[i], P.oy[i], P.oz[i]}, d3{P.dx[i], P.dy[i], P.dz[i]}, P.tm[i]};
-        uint32_t rng = MEDIA ? P.rng[i] : 0u;
-        const hit_state h = world_closest<MEDIA>(S, r, rng);
-        if (MEDIA) P.rng[i] = rng;
+        uint32_t rng = (F & F_MEDIA) ? P.rng[i] : 0u;
+        const hit_state h = world_closest<F>(S, r, rng);
+        if (F & F_MEDIA) P.rng[i] = rng;
         ht[i] = h.t;
         hid[i] = h.prim;
         ++live;
@@ -155,6 +171,7 @@ __device__ __forceinline__ d3 background(const scene& S, const d3& dir) {
 // One segment of color() (RayTracingWeekend.cpp:52-159) for the path in
 // `slot`.  Returns true when the path ends (radiance in L); otherwise the
 // scattered ray / throughput / depth are written back to the slot.
+template <int M>
 __device__ __forceinline__ bool shade_one(const scene& S, const paths_t& P, uint32_t slot, double t, int32_t prim,
                                           d3& L) {
     const ray r{d3{P.ox[slot], P.oy[slot], P.oz[slot]}, d3{P.dx[slot], P.dy[slot], P.dz[slot]}, P.tm[slot]};
@@ -176,13 +193,13 @@ __device__ __forceinline__ bool shade_one(const scene& S, const paths_t& P, uint
     d3 dir;
     d3 f;  // throughput factor of this bounce
     if (m.type == RTW_MAT_DIFFUSE_LIGHT) {  // material.h:232-244: no scatter
-        L = (dot(n, r.d) > 0) ? thr * texture_value(S, m.texture, p) : d3{0, 0, 0};
+        L = (dot(n, r.d) > 0) ? thr * texture_value<M>(S, m.texture, p) : d3{0, 0, 0};
         return true;
-    } else if (m.type == RTW_MAT_METAL) {  // material.h:128-136
+    } else if ((M & SF_METAL) && m.type == RTW_MAT_METAL) {  // material.h:128-136
         const d3 reflected = reflect(normalize(r.d), n);
         dir = reflected + random_in_unit_sphere(rng) * m.fuzz;
         f = ld3(m.albedo);
-    } else if (m.type == RTW_MAT_DIELECTRIC) {  // material.h:146-222
+    } else if ((M & SF_DIEL) && m.type == RTW_MAT_DIELECTRIC) {  // material.h:146-222
         d3 outward;
         double ni_over_nt, cosine;
         const double ri = m.ref_idx;
@@ -201,11 +218,11 @@ __device__ __forceinline__ bool shade_one(const scene& S, const paths_t& P, uint
         const double reflect_prob = refract(r.d, outward, ni_over_nt, refracted) ? schlick(cosine, ri) : 1.0;
         dir = (rnd01(rng) < reflect_prob) ? reflected : refracted;
         f = d3{1.0, 1.0, 1.0};
-    } else if (m.type == RTW_MAT_ISOTROPIC) {  // material.h:257-262
+    } else if ((M & SF_ISO) && m.type == RTW_MAT_ISOTROPIC) {  // material.h:257-262
         dir = random_in_unit_sphere(rng);
-        f = texture_value(S, m.texture, p);
+        f = texture_value<M>(S, m.texture, p);
     } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
-        const d3 att = texture_value(S, m.texture, p);
+        const d3 att = texture_value<M>(S, m.texture, p);
         const onb uvw = onb_from_w(n);
         double pdf_val;
         if (S.n_lights > 0) {  // mixture_pdf(cosine_pdf, hittable_pdf(lights)) pdf.h:55-79
@@ -244,38 +261,115 @@ __device__ __forceinline__ bool shade_one(const scene& S, const paths_t& P, uint
     return false;
 }
 
+// Shade every live path; a path that ends stores its radiance in its sample's
+// slot of the radiance planes and leaves its pool slot empty (depth 0).
+template <int M>
 __global__ __launch_bounds__(kBlock) void k_shade(scene S, job_t J, paths_t P, const double* __restrict__ ht,
                                                   const int32_t* __restrict__ hid, ctrs_t* C) {
-    __shared__ uint32_t s_wave[kWaves];
-    __shared__ unsigned long long s_base;
     const uint32_t n = C->n;
-    const uint32_t stride = gridDim.x * kBlock;
-    for (uint32_t b = blockIdx.x * kBlock; b < n; b += stride) {
-        const uint32_t i = b + threadIdx.x;
-        bool need = false;
-        if (i < n && P.depth[i] != 0) {
-            d3 L;
-            if (shade_one(S, P, i, ht[i], hid[i], L)) {
-                const uint32_t q = P.qid[i];
-                J.Lr[q] = L.x, J.Lg[q] = L.y, J.Lb[q] = L.z;
-                need = true;
-            }
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        if (P.depth[i] == 0) continue;
+        d3 L;
+        if (shade_one<M>(S, P, i, ht[i], hid[i], L)) {
+            const uint32_t q = P.qid[i];
+            J.Lr[q] = L.x, J.Lg[q] = L.y, J.Lb[q] = L.z;
+            P.depth[i] = 0;
         }
-        uint32_t total;
-        const uint32_t rank = block_rank(need, s_wave, total);
-        if (total) {
-            if (threadIdx.x == 0) s_base = atomicAdd(&C->q_next, (unsigned long long)total);
-            __syncthreads();
-            if (need) {
-                const unsigned long long q = s_base + rank;
-                if (q < J.total)
-                    raygen(J, P, i, (uint32_t)q);
-                else
-                    P.depth[i] = 0;  // queue drained: the slot goes dead
-            }
-        }
-        __syncthreads();  // s_wave / s_base reuse
     }
+}
+
+// Block-wide exclusive prefix sum of one value per thread (blockDim = kBlock).
+__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl += y;
+    }
+    if (lane == 63) s_wave[w] = incl;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) {
+        const uint32_t c = s_wave[k];
+        before += (k < (int)w) ? c : 0u;
+        tot += c;
+    }
+    total = tot;
+    return before + incl - v;
+}
+
+// Refill empty pool slots with new camera samples.  Block b owns the slot
+// range [b*kRegenSlots, (b+1)*kRegenSlots): its empty slots are ranked with a
+// block prefix sum into an LDS list (stream compaction), ONE atomic on queue
+// shard b % kQShards reserves that many sample ids, and camera ray-gen then
+// runs densely over the list (no lane idles on a live slot).
+constexpr uint32_t kRegenSlots = 1024;
+
+__global__ __launch_bounds__(kBlock) void k_regen(job_t J, paths_t P, ctrs_t* C) {
+    __shared__ uint32_t s_wave[kWaves];
+    __shared__ uint32_t s_list[kRegenSlots];
+    const uint32_t n = C->n;
+    const uint32_t lo = blockIdx.x * kRegenSlots;
+    if (lo >= n) return;
+    const uint32_t hi = min(n, lo + kRegenSlots);
+    constexpr int kPer = kRegenSlots / kBlock;
+    bool need[kPer];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t i = lo + threadIdx.x + k * kBlock;
+        need[k] = i < hi && P.depth[i] == 0;
+        mine += need[k];
+    }
+    uint32_t total;
+    uint32_t off = block_scan(mine, s_wave, total);
+    if (total == 0) return;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+        if (need[k]) s_list[off++] = lo + threadIdx.x + k * kBlock;
+    // Reserve sample ids: own shard first, then the others while it is dry,
+    // so every shard drains whatever the number of blocks.
+    __shared__ uint32_t s_got[kQShards];
+    __shared__ unsigned long long s_first[kQShards];
+    if (threadIdx.x == 0) {
+        uint32_t left = total;
+        const int own = blockIdx.x % kQShards;
+        for (int a = 0; a < kQShards; ++a) {
+            const int sh = (own + a) % kQShards;
+            s_got[a] = 0;
+            if (left == 0) continue;
+            const unsigned long long lim = shard_limit(sh, J.total);
+            const unsigned long long cur = __hip_atomic_load(&C->qshard[sh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur >= lim) continue;
+            const unsigned long long b = atomicAdd(&C->qshard[sh], (unsigned long long)left);
+            const uint32_t ok = b >= lim ? 0u : (uint32_t)min((unsigned long long)left, lim - b);
+            s_first[a] = b;
+            s_got[a] = ok;
+            left -= ok;
+        }
+    }
+    __syncthreads();
+    const int own = blockIdx.x % kQShards;
+    for (uint32_t e = threadIdx.x; e < total; e += kBlock) {
+        uint32_t k = e;
+        for (int a = 0; a < kQShards; ++a) {
+            if (k < s_got[a]) {
+                const int sh = (own + a) % kQShards;
+                raygen(J, P, s_list[e], (uint32_t)shard_sample(sh, s_first[a] + k));
+                break;
+            }
+            k -= s_got[a];
+        }
+    }
+}
+
+// true once every queue shard has handed out all of its samples
+inline bool queue_drained(const ctrs_t& c, uint32_t total) {
+    for (int s = 0; s < kQShards; ++s)
+        if (c.qshard[s] < shard_limit(s, total)) return false;
+    return true;
 }
 
 // Tail-phase stream compaction of live slots (depth != 0) from A into B.
@@ -378,6 +472,8 @@ struct handle_t {
     hipStream_t stream = nullptr;
     scene S{};
     bool media = false;
+    int features = 0;    // F_MEDIA | F_WBVH | F_GBVH of the uploaded scene
+    int shade_mask = 0;  // SF_* material / texture set of the uploaded scene
     dev_buf scene_mem;
     dev_buf pool[2];  // path SoA, ping-pong for compaction
     dev_buf hits;
@@ -462,7 +558,68 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.n_media = (int32_t)media.size();
     S.has_media = media.empty() ? 0 : 1;
     h->media = !media.empty();
+    h->features = (h->media ? F_MEDIA : 0) | (d->world_bvh_root >= 0 ? F_WBVH : 0);
+    for (int e = 0; e < d->n_entries; ++e)
+        if (d->entries[e].bvh_root >= 0) h->features |= F_GBVH;
+    int m = 0;
+    for (int k = 0; k < d->n_materials; ++k) {
+        const int t = d->materials[k].type;
+        m |= t == RTW_MAT_METAL ? SF_METAL : t == RTW_MAT_DIELECTRIC ? SF_DIEL : t == RTW_MAT_ISOTROPIC ? SF_ISO : 0;
+    }
+    for (int k = 0; k < d->n_textures; ++k) {
+        const int t = d->textures[k].type;
+        m |= t == RTW_TEX_NOISE ? SF_NOISE : t == RTW_TEX_CHECKER ? SF_CHECKER : 0;
+    }
+    h->shade_mask = m;
     return RTW_OK;
+}
+
+// Shade kernels are instantiated for a few material/texture sets; a scene
+// runs the smallest instantiated superset of its own set.
+constexpr int kShadeMasks[] = {SF_DIEL, SF_METAL | SF_DIEL, SF_NOISE, SF_ALL};
+
+void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_t& J, const paths_t& A,
+                  const double* ht, const int32_t* hid, ctrs_t* C) {
+    int pick = SF_ALL;
+    for (int cand : kShadeMasks)
+        if ((mask & ~cand) == 0) {
+            pick = cand;
+            break;
+        }
+    switch (pick) {
+    case SF_DIEL:
+        hipLaunchKernelGGL(k_shade<SF_DIEL>, dim3(grid), dim3(kBlock), 0, st, S, J, A, ht, hid, C);
+        break;
+    case SF_METAL | SF_DIEL:
+        hipLaunchKernelGGL(k_shade<SF_METAL | SF_DIEL>, dim3(grid), dim3(kBlock), 0, st, S, J, A, ht, hid, C);
+        break;
+    case SF_NOISE:
+        hipLaunchKernelGGL(k_shade<SF_NOISE>, dim3(grid), dim3(kBlock), 0, st, S, J, A, ht, hid, C);
+        break;
+    default:
+        hipLaunchKernelGGL(k_shade<SF_ALL>, dim3(grid), dim3(kBlock), 0, st, S, J, A, ht, hid, C);
+    }
+}
+
+// one traversal kernel per scene-feature combination (a world BVH never
+// coexists with media: validate_desc)
+void launch_intersect(int f, int grid, hipStream_t st, const scene& S, const paths_t& A, double* ht, int32_t* hid,
+                      ctrs_t* C) {
+    switch (f) {
+#define RTW_CASE(F)                                                                               \
+    case F:                                                                                       \
+        hipLaunchKernelGGL(k_intersect<F>, dim3(grid), dim3(kBlock), 0, st, S, A, ht, hid, C); \
+        break;
+        RTW_CASE(0)
+        RTW_CASE(F_MEDIA)
+        RTW_CASE(F_WBVH)
+        RTW_CASE(F_GBVH)
+        RTW_CASE(F_MEDIA | F_GBVH)
+        RTW_CASE(F_WBVH | F_GBVH)
+#undef RTW_CASE
+    default:
+        hipLaunchKernelGGL(k_intersect<F_MEDIA | F_GBVH>, dim3(grid), dim3(kBlock), 0, st, S, A, ht, hid, C);
+    }
 }
 
 int validate_desc(const rtw_scene_desc* d) {
@@ -652,6 +809,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     J.Lb = J.Lg + pass_samples;
 
     const int grid = h->grid;
+    const int regen_grid = (int)((pool + kRegenSlots - 1) / kRegenSlots);
     size_t ev = 0;
     std::vector<std::pair<size_t, size_t>> isect_ev, shade_ev;
     hipEvent_t ev_begin = event_at(h, ev++), ev_end = event_at(h, ev++);
@@ -665,11 +823,17 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         J.total = (uint32_t)(S_pass * npix);
         J.s_begin = R.spp_begin + (int)done;
         const uint32_t n0 = std::min<uint32_t>(pool, J.total);
-        hipLaunchKernelGGL(k_fill, dim3((n0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, J, A, C, n0);
+        hipLaunchKernelGGL(k_fill, dim3((n0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, A, C, n0);
+        hipLaunchKernelGGL(k_regen, dim3(regen_grid), dim3(kBlock), 0, st, J, A, C);
         HIPCHK(hipGetLastError());
         bool tail = false;
         std::vector<size_t> checks;  // event slots of status copies, with their copy index
+        // every iteration retires >= 1 live segment; a pass needs at most
+        // total * max_depth / pool + max_depth iterations plus the lag of the
+        // status snapshots -- far beyond that the pool is not draining: fail
+        const uint64_t cap = (uint64_t)J.total * (uint64_t)R.max_depth / n0 + 4ull * R.max_depth + 64;
         for (uint64_t it = 0;; ++it) {
+            if (it > cap) return rtw_fail(RTW_ERR_HIP, "wavefront did not drain (internal error)");
             {
                 size_t e0 = 0, e1 = 0;
                 if (timed) {
@@ -677,10 +841,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                     if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
                     HIPCHK(hipEventRecord(h->events[e0], st));
                 }
-                if (h->media)
-                    hipLaunchKernelGGL(k_intersect<true>, dim3(grid), dim3(kBlock), 0, st, h->S, A, ht, hid, C);
-                else
-                    hipLaunchKernelGGL(k_intersect<false>, dim3(grid), dim3(kBlock), 0, st, h->S, A, ht, hid, C);
+                launch_intersect(h->features, grid, st, h->S, A, ht, hid, C);
                 if (timed) {
                     HIPCHK(hipEventRecord(h->events[e1], st));
                     isect_ev.push_back({e0, e1});
@@ -688,11 +849,12 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                     if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
                     HIPCHK(hipEventRecord(h->events[e0], st));
                 }
-                hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kBlock), 0, st, h->S, J, A, ht, hid, C);
+                launch_shade(h->shade_mask, grid, st, h->S, J, A, ht, hid, C);
                 if (timed) {
                     HIPCHK(hipEventRecord(h->events[e1], st));
                     shade_ev.push_back({e0, e1});
                 }
+                if (!tail) hipLaunchKernelGGL(k_regen, dim3(regen_grid), dim3(kBlock), 0, st, J, A, C);
                 HIPCHK(hipGetLastError());
                 stats.launches_intersect++;
                 stats.iterations++;
@@ -715,7 +877,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 const size_t idx = checks.size() >= 2 ? checks.size() - 2 : 0;
                 HIPCHK(hipEventSynchronize(h->events[checks[idx]]));
                 const ctrs_t snap = h->host_ctrs[idx % 64];
-                if (snap.q_next >= J.total) tail = true;
+                if (queue_drained(snap, J.total)) tail = true;
                 if (tail && snap.n == 0) break;
             }
         }
