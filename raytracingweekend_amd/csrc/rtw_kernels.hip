@@ -261,16 +261,43 @@ __device__ __forceinline__ bool shade_one(const scene& S, const paths_t& P, uint
     return false;
 }
 
+// Re-point a scene's shading arrays into an LDS copy of its prefix.
+__device__ __forceinline__ scene lds_scene(const scene& S, const char* base, const char* lds) {
+    scene L = S;
+    auto rb = [&](const void* p) -> const void* { return p ? (const void*)(lds + ((const char*)p - base)) : nullptr; };
+    L.prims = (const rtw_prim*)rb(S.prims);
+    L.entries = (const rtw_entry*)rb(S.entries);
+    L.materials = (const rtw_material*)rb(S.materials);
+    L.textures = (const rtw_texture*)rb(S.textures);
+    L.lights = (const rtw_light*)rb(S.lights);
+    L.ranvec = (const double*)rb(S.ranvec);
+    L.perm = (const int32_t*)rb(S.perm);
+    L.media = (const int32_t*)rb(S.media);
+    return L;
+}
+
 // Shade every live path; a path that ends stores its radiance in its sample's
 // slot of the radiance planes and leaves its pool slot empty (depth 0).
-template <int M>
+// With LDS, a small scene's shading data (prims .. media, `bytes` from `base`)
+// is staged in LDS once per block: the dependent chain hit -> primitive ->
+// entry -> material -> texture is then LDS latency, not L2 latency.
+template <int M, bool LDS>
 __global__ __launch_bounds__(kBlock) void k_shade(scene S, job_t J, paths_t P, const double* __restrict__ ht,
-                                                  const int32_t* __restrict__ hid, ctrs_t* C) {
+                                                  const int32_t* __restrict__ hid, ctrs_t* C, const char* base,
+                                                  uint32_t bytes) {
+    extern __shared__ __attribute__((aligned(16))) char s_scene[];
+    if (LDS) {
+        const uint4* src = reinterpret_cast<const uint4*>(base);
+        uint4* dst = reinterpret_cast<uint4*>(s_scene);
+        for (uint32_t k = threadIdx.x; k < bytes / 16; k += kBlock) dst[k] = src[k];
+        __syncthreads();
+    }
+    const scene SS = LDS ? lds_scene(S, base, s_scene) : S;
     const uint32_t n = C->n;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         if (P.depth[i] == 0) continue;
         d3 L;
-        if (shade_one<M>(S, P, i, ht[i], hid[i], L)) {
+        if (shade_one<M>(SS, P, i, ht[i], hid[i], L)) {
             const uint32_t q = P.qid[i];
             J.Lr[q] = L.x, J.Lg[q] = L.y, J.Lb[q] = L.z;
             P.depth[i] = 0;
@@ -341,8 +368,11 @@ __global__ __launch_bounds__(kBlock) void k_regen(job_t J, paths_t P, ctrs_t* C)
             s_got[a] = 0;
             if (left == 0) continue;
             const unsigned long long lim = shard_limit(sh, J.total);
-            const unsigned long long cur = __hip_atomic_load(&C->qshard[sh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cur >= lim) continue;
+            if (a > 0) {  // stealing: skip dry shards without an atomic
+                const unsigned long long cur =
+                    __hip_atomic_load(&C->qshard[sh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (cur >= lim) continue;
+            }
             const unsigned long long b = atomicAdd(&C->qshard[sh], (unsigned long long)left);
             const uint32_t ok = b >= lim ? 0u : (uint32_t)min((unsigned long long)left, lim - b);
             s_first[a] = b;
@@ -474,6 +504,8 @@ struct handle_t {
     bool media = false;
     int features = 0;    // F_MEDIA | F_WBVH | F_GBVH of the uploaded scene
     int shade_mask = 0;  // SF_* material / texture set of the uploaded scene
+    const char* scene_base = nullptr;
+    uint32_t shade_bytes = 0;  // bytes of the shading prefix of scene_mem
     dev_buf scene_mem;
     dev_buf pool[2];  // path SoA, ping-pong for compaction
     dev_buf hits;
@@ -515,16 +547,19 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         size_t off;
     };
     std::vector<part> parts = {
+        // parts 0..7 are what shading reads; they come first so a small
+        // scene's shading data is one contiguous prefix the shade kernel can
+        // stage in LDS
         {d->prims, sizeof(rtw_prim) * d->n_prims, 0},
         {d->entries, sizeof(rtw_entry) * d->n_entries, 0},
         {d->materials, sizeof(rtw_material) * d->n_materials, 0},
         {d->textures, sizeof(rtw_texture) * d->n_textures, 0},
         {d->lights, sizeof(rtw_light) * d->n_lights, 0},
-        {d->bvh_nodes, sizeof(rtw_bvh_node) * d->n_bvh_nodes, 0},
-        {d->bvh_items, sizeof(int32_t) * d->n_bvh_items, 0},
         {d->has_perlin ? d->perlin_ranvec : nullptr, d->has_perlin ? sizeof(double) * 768 : 0, 0},
         {d->has_perlin ? d->perlin_perm : nullptr, d->has_perlin ? sizeof(int32_t) * 768 : 0, 0},
         {media.data(), sizeof(int32_t) * media.size(), 0},
+        {d->bvh_nodes, sizeof(rtw_bvh_node) * d->n_bvh_nodes, 0},
+        {d->bvh_items, sizeof(int32_t) * d->n_bvh_items, 0},
     };
     size_t total = 0;
     for (auto& p : parts) {
@@ -545,11 +580,13 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.materials = (const rtw_material*)at(2);
     S.textures = (const rtw_texture*)at(3);
     S.lights = (const rtw_light*)at(4);
-    S.nodes = (const rtw_bvh_node*)at(5);
-    S.items = (const int32_t*)at(6);
-    S.ranvec = (const double*)at(7);
-    S.perm = (const int32_t*)at(8);
-    S.media = (const int32_t*)at(9);
+    S.ranvec = (const double*)at(5);
+    S.perm = (const int32_t*)at(6);
+    S.media = (const int32_t*)at(7);
+    S.nodes = (const rtw_bvh_node*)at(8);
+    S.items = (const int32_t*)at(9);
+    h->shade_bytes = (uint32_t)parts[8].off;  // the shading prefix
+    h->scene_base = base;
     S.n_entries = d->n_entries;
     S.n_lights = d->n_lights;
     S.world_bvh_root = d->world_bvh_root;
@@ -578,26 +615,33 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
 // runs the smallest instantiated superset of its own set.
 constexpr int kShadeMasks[] = {SF_DIEL, SF_METAL | SF_DIEL, SF_NOISE, SF_ALL};
 
+constexpr uint32_t kShadeLdsMax = 40 * 1024;
+
 void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_t& J, const paths_t& A,
-                  const double* ht, const int32_t* hid, ctrs_t* C) {
+                  const double* ht, const int32_t* hid, ctrs_t* C, const char* base, uint32_t bytes) {
     int pick = SF_ALL;
     for (int cand : kShadeMasks)
         if ((mask & ~cand) == 0) {
             pick = cand;
             break;
         }
-    switch (pick) {
-    case SF_DIEL:
-        hipLaunchKernelGGL(k_shade<SF_DIEL>, dim3(grid), dim3(kBlock), 0, st, S, J, A, ht, hid, C);
+    const bool lds = bytes <= kShadeLdsMax;
+    const size_t shm = lds ? bytes : 0;
+    switch (pick * 2 + (lds ? 1 : 0)) {
+#define RTW_CASE(M, LDS)                                                                                   \
+    case M * 2 + (LDS ? 1 : 0):                                                                            \
+        hipLaunchKernelGGL((k_shade<M, LDS>), dim3(grid), dim3(kBlock), shm, st, S, J, A, ht, hid, C, base, bytes); \
         break;
-    case SF_METAL | SF_DIEL:
-        hipLaunchKernelGGL(k_shade<SF_METAL | SF_DIEL>, dim3(grid), dim3(kBlock), 0, st, S, J, A, ht, hid, C);
-        break;
-    case SF_NOISE:
-        hipLaunchKernelGGL(k_shade<SF_NOISE>, dim3(grid), dim3(kBlock), 0, st, S, J, A, ht, hid, C);
-        break;
+        RTW_CASE(SF_DIEL, true)
+        RTW_CASE(SF_DIEL, false)
+        RTW_CASE(SF_METAL | SF_DIEL, true)
+        RTW_CASE(SF_METAL | SF_DIEL, false)
+        RTW_CASE(SF_NOISE, true)
+        RTW_CASE(SF_NOISE, false)
+        RTW_CASE(SF_ALL, true)
+#undef RTW_CASE
     default:
-        hipLaunchKernelGGL(k_shade<SF_ALL>, dim3(grid), dim3(kBlock), 0, st, S, J, A, ht, hid, C);
+        hipLaunchKernelGGL((k_shade<SF_ALL, false>), dim3(grid), dim3(kBlock), 0, st, S, J, A, ht, hid, C, base, bytes);
     }
 }
 
@@ -849,7 +893,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                     if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
                     HIPCHK(hipEventRecord(h->events[e0], st));
                 }
-                launch_shade(h->shade_mask, grid, st, h->S, J, A, ht, hid, C);
+                launch_shade(h->shade_mask, grid, st, h->S, J, A, ht, hid, C, h->scene_base, h->shade_bytes);
                 if (timed) {
                     HIPCHK(hipEventRecord(h->events[e1], st));
                     shade_ev.push_back({e0, e1});
