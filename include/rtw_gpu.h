@@ -217,7 +217,8 @@ typedef struct rtw_render_params {
     int32_t row_begin;     /* ... of rows j = row_begin + k*row_step (pixel sharding) */
     int32_t row_step;      /* 0 or 1 = every row                                    */
     int32_t accum_on_device; /* 1: accum_rgb is a device pointer on this handle's GPU */
-    int32_t collect_kernel_times; /* 1: bracket every launch with hipEvents      */
+    int32_t collect_kernel_times; /* 1: hipEvents around traversal launches,    */
+                                  /* 2: and shade launches (adds queue gaps)   */
     int32_t wavefront_paths; /* paths in flight (0 = library default)             */
     int32_t reserved;
 } rtw_render_params;

@@ -5,14 +5,17 @@
 // of color() (RayTracingWeekend.cpp:45-160) is unrolled into an iterative
 // wavefront over a pool of in-flight paths kept as SoA arrays in HBM:
 //
-//   k_fill       camera ray-gen for the first min(P, samples) samples
+//   k_fill + k_regen   empty pool, then camera ray-gen for the first samples
 //   repeat:
 //     k_intersect  one world closest-hit query per live path   (traversal)
 //     k_shade      emission / scatter / mixture-pdf sampling per path; a
-//                  path that ends writes its radiance to its sample's slot of
-//                  the per-sample radiance planes and its pool slot is refilled
-//                  with a new camera sample from a block-aggregated queue
-//                  (__ballot + popcount prefix, one atomic per 256 paths)
+//                  path that ends writes its 24-byte radiance record to its
+//                  sample's slot of the pass's radiance buffer and empties
+//                  its pool slot
+//     k_regen      (until the sample queue is drained) refills empty slots:
+//                  per-block compaction of the empty slots, one atomic on a
+//                  sharded sample queue per 1024 slots, camera rays written
+//                  densely to a staging buffer, a 4-byte marker per slot
 //     k_compact    (tail only, once the sample queue is drained) stream
 //                  compaction of live paths, __ballot/prefix-sum per tile
 //   k_reduce     per-pixel sum of the samples in increasing sample order
@@ -35,9 +38,22 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 
+// Path pool (SoA, one element per slot).  depth word of a slot:
+//   0                    empty
+//   1..max_depth         live path: the depth argument of its next color() call
+//   kFresh | k           a new camera sample whose ray / time / rng / sample id
+//                        sit in staging entry k (written densely by k_regen);
+//                        its throughput is 1 and its depth max_depth
+constexpr uint32_t kFresh = 0x80000000u;
+
 struct paths_t {
     double *ox, *oy, *oz, *dx, *dy, *dz, *tm, *tr, *tg, *tb;
     uint32_t *rng, *depth, *qid;
+};
+
+struct fresh_t {  // staging of new camera rays, indexed like the pool
+    double *ox, *oy, *oz, *dx, *dy, *dz, *tm;
+    uint32_t *rng, *qid;
 };
 
 // The sample queue is sharded over kQShards counters to spread the atomics:
@@ -47,9 +63,18 @@ struct paths_t {
 constexpr int kQShards = 8;
 constexpr uint32_t kQChunk = 1024;
 
+// Counters hit by many workgroups live on 256-byte lines of their own: all
+// words of one line are served by one L2 channel, which serialises them
+// (one word saturates at ~88 atomics/us).  Shard k is used by the blocks with
+// blockIdx % 8 == k, i.e. by one XCD.
+struct alignas(256) ctr_line {
+    unsigned long long v;
+    unsigned long long pad[31];
+};
+
 struct ctrs_t {
-    unsigned long long qshard[kQShards]; // per-shard count of samples handed out
-    unsigned long long segments;         // world hit queries (live paths intersected)
+    ctr_line qshard[kQShards];  // per-shard count of samples handed out
+    ctr_line segments[8];       // world hit queries (live paths intersected)
     unsigned int n;                      // slots in the current pool
     unsigned int n_out;                  // compaction output count
     unsigned int pad[4];
@@ -71,7 +96,7 @@ struct job_t {
     uint32_t total;      // samples in this pass
     uint32_t npix;       // pixels of this call (n_rows * nx)
     int32_t nx, ny, row_begin, row_step, s_begin, max_depth;
-    double *Lr, *Lg, *Lb; // per-sample radiance, index q (pass-local sample id)
+    double* L;           // per-sample radiance, L[3q + c] (pass-local sample id q)
 };
 
 // pass-local sample id -> pixel (i, j) and global sample index s
@@ -85,21 +110,44 @@ __device__ __forceinline__ void sample_coords(const job_t& J, uint32_t q, int& i
 }
 
 // Render-loop body RayTracingWeekend.cpp:227-231 for sample q: jitter,
-// camera::get_ray; throughput 1, depth = max_depth.
-__device__ __forceinline__ void raygen(const job_t& J, const paths_t& P, uint32_t slot, uint32_t q) {
+// camera::get_ray -> staging entry k.
+__device__ __forceinline__ void raygen(const job_t& J, const fresh_t& F, uint32_t k, uint32_t q) {
     int i, j, s;
     sample_coords(J, q, i, j, s);
     uint32_t rng = path_seed(J.seed_mix, (uint32_t)(j * J.nx + i), (uint32_t)s);
     const double u = (double)(i + rnd01(rng)) / (double)J.nx;
     const double v = (double)(j + rnd01(rng)) / (double)J.ny;
     const ray r = camera_ray(J.cam, u, v, rng);
-    P.ox[slot] = r.o.x, P.oy[slot] = r.o.y, P.oz[slot] = r.o.z;
-    P.dx[slot] = r.d.x, P.dy[slot] = r.d.y, P.dz[slot] = r.d.z;
-    P.tm[slot] = r.t;
-    P.tr[slot] = 1.0, P.tg[slot] = 1.0, P.tb[slot] = 1.0;
-    P.rng[slot] = rng;
-    P.depth[slot] = (uint32_t)J.max_depth;
-    P.qid[slot] = q;
+    F.ox[k] = r.o.x, F.oy[k] = r.o.y, F.oz[k] = r.o.z;
+    F.dx[k] = r.d.x, F.dy[k] = r.d.y, F.dz[k] = r.d.z;
+    F.tm[k] = r.t;
+    F.rng[k] = rng;
+    F.qid[k] = q;
+}
+
+// A path as the kernels see it: from the pool, or from staging when fresh.
+struct path_in {
+    ray r;
+    uint32_t depth;
+    bool fresh;
+    uint32_t src;  // staging index (fresh) or pool slot
+};
+
+__device__ __forceinline__ path_in load_ray(const paths_t& P, const fresh_t& F, uint32_t i, uint32_t dw) {
+    path_in x;
+    x.fresh = (dw & kFresh) != 0;
+    x.src = x.fresh ? (dw & ~kFresh) : i;
+    // one load per field with a per-lane address: no divergence between
+    // fresh and continuing paths
+    x.r.o.x = *(x.fresh ? F.ox + x.src : P.ox + i);
+    x.r.o.y = *(x.fresh ? F.oy + x.src : P.oy + i);
+    x.r.o.z = *(x.fresh ? F.oz + x.src : P.oz + i);
+    x.r.d.x = *(x.fresh ? F.dx + x.src : P.dx + i);
+    x.r.d.y = *(x.fresh ? F.dy + x.src : P.dy + i);
+    x.r.d.z = *(x.fresh ? F.dz + x.src : P.dz + i);
+    x.r.t = *(x.fresh ? F.tm + x.src : P.tm + i);
+    x.depth = dw;
+    return x;
 }
 
 // Start a pass: slots [0, n0) empty (depth 0) for k_regen to fill.
@@ -107,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_fill(paths_t P, ctrs_t* C, uint32_t 
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i < n0) P.depth[i] = 0;
     if (i == 0) C->n = n0;
-    if (i < kQShards) C->qshard[i] = 0;
+    if (i < kQShards) C->qshard[i].v = 0;
 }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() {
@@ -133,21 +181,39 @@ __device__ __forceinline__ uint32_t block_rank(bool flag, uint32_t* s_wave, uint
     return before + (uint32_t)__popcll(m & lanemask_lt());
 }
 
+// One world closest-hit query per live path.  The next path's ray is loaded
+// while the current one is traversed (software pipelining of the HBM reads).
 template <int F>
-__global__ __launch_bounds__(kBlock) void k_intersect(scene S, paths_t P, double* __restrict__ ht,
+__global__ __launch_bounds__(kBlock) void k_intersect(scene S, paths_t P, fresh_t FR, double* __restrict__ ht,
                                                       int32_t* __restrict__ hid, ctrs_t* C) {
     __shared__ uint32_t s_cnt[kWaves];
     const uint32_t n = C->n;
+    const uint32_t stride = gridDim.x * kBlock;
     uint32_t live = 0;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        if (P.depth[i] == 0) continue;
-        const ray r{d3{P.ox[i], P.oy[i], P.oz[i]}, d3{P.dx[i], P.dy[i], P.dz[i]}, P.tm[i]};
-        uint32_t rng = (F & F_MEDIA) ? P.rng[i] : 0u;
-        const hit_state h = world_closest<F>(S, r, rng);
-        if (F & F_MEDIA) P.rng[i] = rng;
-        ht[i] = h.t;
-        hid[i] = h.prim;
-        ++live;
+    uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    uint32_t dw = i < n ? P.depth[i] : 0u;
+    path_in cur = load_ray(P, FR, i < n ? i : 0, dw);
+    while (i < n) {
+        const uint32_t nx = i + stride;
+        const uint32_t ndw = nx < n ? P.depth[nx] : 0u;
+        const path_in nxt = load_ray(P, FR, nx < n ? nx : i, ndw);
+        if (dw != 0) {
+            uint32_t rng = 0u;
+            if (F & F_MEDIA) rng = cur.fresh ? FR.rng[cur.src] : P.rng[i];
+            const hit_state h = world_closest<F>(S, cur.r, rng);
+            if (F & F_MEDIA) {
+                if (cur.fresh)
+                    FR.rng[cur.src] = rng;
+                else
+                    P.rng[i] = rng;
+            }
+            ht[i] = h.t;
+            hid[i] = h.prim;
+            ++live;
+        }
+        i = nx;
+        dw = ndw;
+        cur = nxt;
     }
     // one 64-bit atomic per block for the segment counter
     for (int off = 32; off > 0; off >>= 1) live += __shfl_down(live, off, 64);
@@ -156,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void k_intersect(scene S, paths_t P, double
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
         for (int k = 0; k < kWaves; ++k) t += s_cnt[k];
-        if (t) atomicAdd(&C->segments, t);
+        if (t) atomicAdd(&C->segments[blockIdx.x % 8].v, t);
     }
 }
 
@@ -168,14 +234,19 @@ __device__ __forceinline__ d3 background(const scene& S, const d3& dir) {
     return d3{1.0, 1.0, 1.0} * (1.0 - t) + d3{0.5f, 0.7f, 1.0} * t;  // lerp, vec3.h:84-87
 }
 
-// One segment of color() (RayTracingWeekend.cpp:52-159) for the path in
-// `slot`.  Returns true when the path ends (radiance in L); otherwise the
-// scattered ray / throughput / depth are written back to the slot.
+// One segment of color() (RayTracingWeekend.cpp:52-159) for the path x in
+// pool slot i, whose world hit is (t, prim) and whose engine state is rng.
+// Returns true when the path ends (radiance in L); otherwise the scattered
+// ray, throughput, rng and depth are written to the slot (which stops being
+// fresh).
 template <int M>
-__device__ __forceinline__ bool shade_one(const scene& S, const paths_t& P, uint32_t slot, double t, int32_t prim,
-                                          d3& L) {
-    const ray r{d3{P.ox[slot], P.oy[slot], P.oz[slot]}, d3{P.dx[slot], P.dy[slot], P.dz[slot]}, P.tm[slot]};
-    const d3 thr{P.tr[slot], P.tg[slot], P.tb[slot]};
+__device__ __forceinline__ bool shade_one(const scene& S, const job_t& J, const paths_t& P, const fresh_t& FR,
+                                          uint32_t i, const path_in& x, uint32_t rng, double t, int32_t prim, d3& L,
+                                          uint32_t& q) {
+    const uint32_t dw = x.depth;
+    const ray& r = x.r;
+    const d3 thr = x.fresh ? d3{1.0, 1.0, 1.0} : d3{P.tr[i], P.tg[i], P.tb[i]};
+    q = x.fresh ? FR.qid[x.src] : P.qid[i];
     if (prim == -1) {
         L = thr * background(S, r.d);
         return true;
@@ -188,8 +259,7 @@ __device__ __forceinline__ bool shade_one(const scene& S, const paths_t& P, uint
         return true;
     }
     const rtw_material& m = S.materials[mat];
-    uint32_t rng = P.rng[slot];
-    const uint32_t depth = P.depth[slot];
+    const uint32_t depth = x.fresh ? (uint32_t)J.max_depth : dw;
     d3 dir;
     d3 f;  // throughput factor of this bounce
     if (m.type == RTW_MAT_DIFFUSE_LIGHT) {  // material.h:232-244: no scatter
@@ -232,13 +302,13 @@ __device__ __forceinline__ bool shade_one(const scene& S, const paths_t& P, uint
                 const int k = random_int(rng, 0, S.n_lights - 1);
                 dir = light_random(S, S.lights[k], p, rng);
             }
-            const double c = dot(normalize(dir), uvw.w);
-            const double p0 = (c <= 0) ? 0 : c / kPi;
+            const double cw = dot(normalize(dir), uvw.w);
+            const double p0 = (cw <= 0) ? 0 : cw / kPi;
             pdf_val = 0.5 * p0 + 0.5 * lights_pdf_value(S, p, dir);
         } else {
             dir = local(uvw, random_cosine_direction(rng));
-            const double c = dot(normalize(dir), uvw.w);
-            pdf_val = (c <= 0) ? 0 : c / kPi;
+            const double cw = dot(normalize(dir), uvw.w);
+            pdf_val = (cw <= 0) ? 0 : cw / kPi;
         }
         if (pdf_val <= 0.0) {  // :126-127 returns emitted (= 0)
             L = d3{0, 0, 0};
@@ -253,11 +323,13 @@ __device__ __forceinline__ bool shade_one(const scene& S, const paths_t& P, uint
         return true;
     }
     const d3 nt = thr * f;
-    P.ox[slot] = p.x, P.oy[slot] = p.y, P.oz[slot] = p.z;
-    P.dx[slot] = dir.x, P.dy[slot] = dir.y, P.dz[slot] = dir.z;
-    P.tr[slot] = nt.x, P.tg[slot] = nt.y, P.tb[slot] = nt.z;
-    P.rng[slot] = rng;
-    P.depth[slot] = depth - 1;
+    P.ox[i] = p.x, P.oy[i] = p.y, P.oz[i] = p.z;
+    P.dx[i] = dir.x, P.dy[i] = dir.y, P.dz[i] = dir.z;
+    P.tm[i] = r.t;
+    P.tr[i] = nt.x, P.tg[i] = nt.y, P.tb[i] = nt.z;
+    P.rng[i] = rng;
+    P.depth[i] = depth - 1;
+    P.qid[i] = q;
     return false;
 }
 
@@ -277,14 +349,14 @@ __device__ __forceinline__ scene lds_scene(const scene& S, const char* base, con
 }
 
 // Shade every live path; a path that ends stores its radiance in its sample's
-// slot of the radiance planes and leaves its pool slot empty (depth 0).
+// slot of the radiance buffer (one 24-byte record) and empties its pool slot.
 // With LDS, a small scene's shading data (prims .. media, `bytes` from `base`)
 // is staged in LDS once per block: the dependent chain hit -> primitive ->
 // entry -> material -> texture is then LDS latency, not L2 latency.
 template <int M, bool LDS>
-__global__ __launch_bounds__(kBlock) void k_shade(scene S, job_t J, paths_t P, const double* __restrict__ ht,
-                                                  const int32_t* __restrict__ hid, ctrs_t* C, const char* base,
-                                                  uint32_t bytes) {
+__global__ __launch_bounds__(kBlock) void k_shade(scene S, job_t J, paths_t P, fresh_t FR,
+                                                  const double* __restrict__ ht, const int32_t* __restrict__ hid,
+                                                  ctrs_t* C, const char* base, uint32_t bytes) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     if (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(base);
@@ -295,13 +367,59 @@ __global__ __launch_bounds__(kBlock) void k_shade(scene S, job_t J, paths_t P, c
     const scene SS = LDS ? lds_scene(S, base, s_scene) : S;
     const uint32_t n = C->n;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        if (P.depth[i] == 0) continue;
+        const uint32_t dw = P.depth[i];
+        if (dw == 0) continue;
         d3 L;
-        if (shade_one<M>(SS, P, i, ht[i], hid[i], L)) {
-            const uint32_t q = P.qid[i];
-            J.Lr[q] = L.x, J.Lg[q] = L.y, J.Lb[q] = L.z;
+        uint32_t q;
+        const path_in x = load_ray(P, FR, i, dw);
+        const uint32_t rng = x.fresh ? FR.rng[x.src] : P.rng[i];
+        if (shade_one<M>(SS, J, P, FR, i, x, rng, ht[i], hid[i], L, q)) {
+            double* o = J.L + 3 * (size_t)q;
+            o[0] = L.x, o[1] = L.y, o[2] = L.z;
             P.depth[i] = 0;
         }
+    }
+}
+
+// Fused segment: traversal + shading of each live path in one pass over the
+// pool (the ray is read once; no hit records go through HBM).  Same results
+// as k_intersect followed by k_shade.
+template <int F, int M, bool LDS>
+__global__ __launch_bounds__(kBlock) void k_segment(scene S, job_t J, paths_t P, fresh_t FR, ctrs_t* C,
+                                                    const char* base, uint32_t bytes) {
+    extern __shared__ __attribute__((aligned(16))) char s_scene[];
+    __shared__ uint32_t s_cnt[kWaves];
+    if (LDS) {
+        const uint4* src = reinterpret_cast<const uint4*>(base);
+        uint4* dst = reinterpret_cast<uint4*>(s_scene);
+        for (uint32_t k = threadIdx.x; k < bytes / 16; k += kBlock) dst[k] = src[k];
+        __syncthreads();
+    }
+    const scene SS = LDS ? lds_scene(S, base, s_scene) : S;
+    const uint32_t n = C->n;
+    uint32_t live = 0;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const uint32_t dw = P.depth[i];
+        if (dw == 0) continue;
+        const path_in x = load_ray(P, FR, i, dw);
+        uint32_t rng = x.fresh ? FR.rng[x.src] : P.rng[i];
+        const hit_state h = world_closest<F>(S, x.r, rng);
+        ++live;
+        d3 L;
+        uint32_t q;
+        if (shade_one<M>(SS, J, P, FR, i, x, rng, h.t, h.prim, L, q)) {
+            double* o = J.L + 3 * (size_t)q;
+            o[0] = L.x, o[1] = L.y, o[2] = L.z;
+            P.depth[i] = 0;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) live += __shfl_down(live, off, 64);
+    if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = live;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int k = 0; k < kWaves; ++k) t += s_cnt[k];
+        if (t) atomicAdd(&C->segments[blockIdx.x % 8].v, t);
     }
 }
 
@@ -328,13 +446,16 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* s_wave, uin
 }
 
 // Refill empty pool slots with new camera samples.  Block b owns the slot
-// range [b*kRegenSlots, (b+1)*kRegenSlots): its empty slots are ranked with a
-// block prefix sum into an LDS list (stream compaction), ONE atomic on queue
-// shard b % kQShards reserves that many sample ids, and camera ray-gen then
-// runs densely over the list (no lane idles on a live slot).
+// range [lo, lo + kRegenSlots): its empty slots are ranked with a block prefix
+// sum into an LDS list (stream compaction), ONE atomic on queue shard
+// b % kQShards reserves that many sample ids, ray-gen runs densely over the
+// list and writes the rays DENSELY to staging entries lo, lo+1, ...; each empty
+// slot only receives its 4-byte fresh marker.  (Scattered 8-byte stores into
+// pool lines that have left L2 cost a memory-side read-modify-write each:
+// measured 52 us vs 5 us per launch for 13 scattered arrays vs 3.)
 constexpr uint32_t kRegenSlots = 1024;
 
-__global__ __launch_bounds__(kBlock) void k_regen(job_t J, paths_t P, ctrs_t* C) {
+__global__ __launch_bounds__(kBlock) void k_regen(job_t J, paths_t P, fresh_t FR, ctrs_t* C) {
     __shared__ uint32_t s_wave[kWaves];
     __shared__ uint32_t s_list[kRegenSlots];
     const uint32_t n = C->n;
@@ -370,10 +491,10 @@ __global__ __launch_bounds__(kBlock) void k_regen(job_t J, paths_t P, ctrs_t* C)
             const unsigned long long lim = shard_limit(sh, J.total);
             if (a > 0) {  // stealing: skip dry shards without an atomic
                 const unsigned long long cur =
-                    __hip_atomic_load(&C->qshard[sh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_load(&C->qshard[sh].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (cur >= lim) continue;
             }
-            const unsigned long long b = atomicAdd(&C->qshard[sh], (unsigned long long)left);
+            const unsigned long long b = atomicAdd(&C->qshard[sh].v, (unsigned long long)left);
             const uint32_t ok = b >= lim ? 0u : (uint32_t)min((unsigned long long)left, lim - b);
             s_first[a] = b;
             s_got[a] = ok;
@@ -387,7 +508,8 @@ __global__ __launch_bounds__(kBlock) void k_regen(job_t J, paths_t P, ctrs_t* C)
         for (int a = 0; a < kQShards; ++a) {
             if (k < s_got[a]) {
                 const int sh = (own + a) % kQShards;
-                raygen(J, P, s_list[e], (uint32_t)shard_sample(sh, s_first[a] + k));
+                raygen(J, FR, lo + e, (uint32_t)shard_sample(sh, s_first[a] + k));
+                P.depth[s_list[e]] = kFresh | (lo + e);
                 break;
             }
             k -= s_got[a];
@@ -398,11 +520,12 @@ __global__ __launch_bounds__(kBlock) void k_regen(job_t J, paths_t P, ctrs_t* C)
 // true once every queue shard has handed out all of its samples
 inline bool queue_drained(const ctrs_t& c, uint32_t total) {
     for (int s = 0; s < kQShards; ++s)
-        if (c.qshard[s] < shard_limit(s, total)) return false;
+        if (c.qshard[s].v < shard_limit(s, total)) return false;
     return true;
 }
 
-// Tail-phase stream compaction of live slots (depth != 0) from A into B.
+// Tail-phase stream compaction of live slots (depth != 0) from A into B
+// (fresh markers move with their slot; staging is not rewritten in the tail).
 __global__ __launch_bounds__(kBlock) void k_compact(paths_t A, paths_t B, ctrs_t* C) {
     __shared__ uint32_t s_wave[kWaves];
     __shared__ uint32_t s_base;
@@ -434,16 +557,15 @@ __global__ void k_commit(ctrs_t* C) {
 }
 
 // running[pix] += L[s][pix] for s = 0..S-1 in order (RayTracingWeekend.cpp:235-239)
-__global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ Lr, const double* __restrict__ Lg,
-                                                   const double* __restrict__ Lb, uint32_t npix, uint32_t spp,
+__global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ L, uint32_t npix, uint32_t spp,
                                                    double* __restrict__ run) {
     for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < npix; p += gridDim.x * kBlock) {
         double r = run[3 * p], g = run[3 * p + 1], bl = run[3 * p + 2];
         for (uint32_t s = 0; s < spp; ++s) {
-            const size_t q = (size_t)s * npix + p;
-            r = r + Lr[q];
-            g = g + Lg[q];
-            bl = bl + Lb[q];
+            const double* x = L + 3 * ((size_t)s * npix + p);
+            r = r + x[0];
+            g = g + x[1];
+            bl = bl + x[2];
         }
         run[3 * p] = r, run[3 * p + 1] = g, run[3 * p + 2] = bl;
     }
@@ -508,6 +630,7 @@ struct handle_t {
     uint32_t shade_bytes = 0;  // bytes of the shading prefix of scene_mem
     dev_buf scene_mem;
     dev_buf pool[2];  // path SoA, ping-pong for compaction
+    dev_buf fresh;    // staging of new camera rays (fresh_t)
     dev_buf hits;
     dev_buf radiance; // per-sample planes of one pass
     dev_buf run;      // per-pixel running sums
@@ -535,6 +658,20 @@ paths_t carve_paths(void* base, uint32_t cap) {
     return P;
 }
 size_t paths_bytes(uint32_t cap) { return (size_t)cap * (10 * 8 + 3 * 4); }
+
+fresh_t carve_fresh(void* base, uint32_t cap) {
+    char* p = static_cast<char*>(base);
+    fresh_t F;
+    double** d[] = {&F.ox, &F.oy, &F.oz, &F.dx, &F.dy, &F.dz, &F.tm};
+    for (double** x : d) {
+        *x = reinterpret_cast<double*>(p);
+        p += (size_t)cap * 8;
+    }
+    F.rng = reinterpret_cast<uint32_t*>(p);
+    F.qid = F.rng + cap;
+    return F;
+}
+size_t fresh_bytes(uint32_t cap) { return (size_t)cap * (7 * 8 + 2 * 4); }
 
 int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     // one allocation, 256-byte aligned sub-arrays
@@ -617,20 +754,45 @@ constexpr int kShadeMasks[] = {SF_DIEL, SF_METAL | SF_DIEL, SF_NOISE, SF_ALL};
 
 constexpr uint32_t kShadeLdsMax = 40 * 1024;
 
-void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_t& J, const paths_t& A,
-                  const double* ht, const int32_t* hid, ctrs_t* C, const char* base, uint32_t bytes) {
-    int pick = SF_ALL;
+int pick_shade_mask(int mask) {
     for (int cand : kShadeMasks)
-        if ((mask & ~cand) == 0) {
-            pick = cand;
-            break;
-        }
+        if ((mask & ~cand) == 0) return cand;
+    return SF_ALL;
+}
+
+// Fused traversal + shading for the common scene shapes; returns false when
+// no fused instantiation covers (features, material set), and the caller
+// then runs the split k_intersect / k_shade pair.  probe: only report.
+bool launch_segment(bool probe, int f, int mask, int grid, hipStream_t st, const scene& S, const job_t& J,
+                    const paths_t& A, const fresh_t& FR, ctrs_t* C, const char* base, uint32_t bytes) {
+    const int pick = pick_shade_mask(mask);
+    const bool lds = bytes <= kShadeLdsMax;
+    const size_t shm = lds ? bytes : 0;
+#define RTW_SEG(FF, MM, LL)                                                                                    \
+    if (f == (FF) && pick == (MM) && lds == (LL)) {                                                          \
+        if (!probe)                                                                                           \
+            hipLaunchKernelGGL((k_segment<FF, MM, LL>), dim3(grid), dim3(kBlock), shm, st, S, J, A, FR, C, base, bytes); \
+        return true;                                                                                         \
+    }
+    RTW_SEG(0, SF_DIEL, true)
+    RTW_SEG(0, SF_METAL | SF_DIEL, true)
+    RTW_SEG(0, SF_ALL, true)
+    RTW_SEG(0, SF_ALL, false)
+    RTW_SEG(F_WBVH, SF_ALL, false)
+    RTW_SEG(F_WBVH, SF_ALL, true)
+#undef RTW_SEG
+    return false;
+}
+
+void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_t& J, const paths_t& A,
+                  const fresh_t& F, const double* ht, const int32_t* hid, ctrs_t* C, const char* base, uint32_t bytes) {
+    const int pick = pick_shade_mask(mask);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
     switch (pick * 2 + (lds ? 1 : 0)) {
 #define RTW_CASE(M, LDS)                                                                                   \
     case M * 2 + (LDS ? 1 : 0):                                                                            \
-        hipLaunchKernelGGL((k_shade<M, LDS>), dim3(grid), dim3(kBlock), shm, st, S, J, A, ht, hid, C, base, bytes); \
+        hipLaunchKernelGGL((k_shade<M, LDS>), dim3(grid), dim3(kBlock), shm, st, S, J, A, F, ht, hid, C, base, bytes); \
         break;
         RTW_CASE(SF_DIEL, true)
         RTW_CASE(SF_DIEL, false)
@@ -641,18 +803,19 @@ void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_
         RTW_CASE(SF_ALL, true)
 #undef RTW_CASE
     default:
-        hipLaunchKernelGGL((k_shade<SF_ALL, false>), dim3(grid), dim3(kBlock), 0, st, S, J, A, ht, hid, C, base, bytes);
+        hipLaunchKernelGGL((k_shade<SF_ALL, false>), dim3(grid), dim3(kBlock), 0, st, S, J, A, F, ht, hid, C, base, bytes);
     }
 }
 
 // one traversal kernel per scene-feature combination (a world BVH never
 // coexists with media: validate_desc)
-void launch_intersect(int f, int grid, hipStream_t st, const scene& S, const paths_t& A, double* ht, int32_t* hid,
+void launch_intersect(int f, int grid, hipStream_t st, const scene& S, const paths_t& A, const fresh_t& FR,
+                      double* ht, int32_t* hid,
                       ctrs_t* C) {
     switch (f) {
 #define RTW_CASE(F)                                                                               \
     case F:                                                                                       \
-        hipLaunchKernelGGL(k_intersect<F>, dim3(grid), dim3(kBlock), 0, st, S, A, ht, hid, C); \
+        hipLaunchKernelGGL(k_intersect<F>, dim3(grid), dim3(kBlock), 0, st, S, A, FR, ht, hid, C); \
         break;
         RTW_CASE(0)
         RTW_CASE(F_MEDIA)
@@ -662,7 +825,7 @@ void launch_intersect(int f, int grid, hipStream_t st, const scene& S, const pat
         RTW_CASE(F_WBVH | F_GBVH)
 #undef RTW_CASE
     default:
-        hipLaunchKernelGGL(k_intersect<F_MEDIA | F_GBVH>, dim3(grid), dim3(kBlock), 0, st, S, A, ht, hid, C);
+        hipLaunchKernelGGL(k_intersect<F_MEDIA | F_GBVH>, dim3(grid), dim3(kBlock), 0, st, S, A, FR, ht, hid, C);
     }
 }
 
@@ -780,6 +943,7 @@ extern "C" void rtw_scene_free(void* handle) {
     h->scene_mem.release();
     h->pool[0].release();
     h->pool[1].release();
+    h->fresh.release();
     h->hits.release();
     h->radiance.release();
     h->run.release();
@@ -831,10 +995,12 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     int rc;
     if ((rc = h->pool[0].ensure(paths_bytes(pool)))) return rc;
     if ((rc = h->pool[1].ensure(paths_bytes(pool)))) return rc;
+    if ((rc = h->fresh.ensure(fresh_bytes(pool)))) return rc;
     if ((rc = h->hits.ensure((size_t)pool * 12))) return rc;
     if ((rc = h->radiance.ensure(pass_samples * 24))) return rc;
     if ((rc = h->run.ensure(npix * 24))) return rc;
     paths_t A = carve_paths(h->pool[0].p, pool), B = carve_paths(h->pool[1].p, pool);
+    const fresh_t FR = carve_fresh(h->fresh.p, pool);
     double* ht = static_cast<double*>(h->hits.p);
     int32_t* hid = reinterpret_cast<int32_t*>(static_cast<char*>(h->hits.p) + (size_t)pool * 8);
     ctrs_t* C = static_cast<ctrs_t*>(h->ctrs.p);
@@ -848,9 +1014,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     J.npix = (uint32_t)npix;
     J.nx = R.nx, J.ny = R.ny, J.row_begin = R.row_begin, J.row_step = row_step;
     J.max_depth = R.max_depth;
-    J.Lr = static_cast<double*>(h->radiance.p);
-    J.Lg = J.Lr + pass_samples;
-    J.Lb = J.Lg + pass_samples;
+    J.L = static_cast<double*>(h->radiance.p);
 
     const int grid = h->grid;
     const int regen_grid = (int)((pool + kRegenSlots - 1) / kRegenSlots);
@@ -859,7 +1023,17 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     hipEvent_t ev_begin = event_at(h, ev++), ev_end = event_at(h, ev++);
     if (!ev_begin || !ev_end) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
     HIPCHK(hipEventRecord(ev_begin, st));
+    // collect_kernel_times: 1 = events around each traversal launch (the
+    // roofline kernel), 2 = also around each shade launch.  Every event pair
+    // costs a few us of queue gap per iteration, so the default is neither.
     const bool timed = R.collect_kernel_times != 0;
+    const bool timed_shade = R.collect_kernel_times >= 2;
+    // traversal + shading fused into one kernel where an instantiation covers
+    // the scene (RTW_SPLIT=1 forces the split pair, for tests and profiling)
+    const char* split_env = std::getenv("RTW_SPLIT");
+    const bool fused = !(split_env && std::atoi(split_env) != 0) &&
+                       launch_segment(true, h->features, h->shade_mask, 0, st, h->S, J, A, FR, C, h->scene_base,
+                                      h->shade_bytes);
     const int check_every = 4;
 
     for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
@@ -868,7 +1042,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         J.s_begin = R.spp_begin + (int)done;
         const uint32_t n0 = std::min<uint32_t>(pool, J.total);
         hipLaunchKernelGGL(k_fill, dim3((n0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, A, C, n0);
-        hipLaunchKernelGGL(k_regen, dim3(regen_grid), dim3(kBlock), 0, st, J, A, C);
+        hipLaunchKernelGGL(k_regen, dim3(regen_grid), dim3(kBlock), 0, st, J, A, FR, C);
         HIPCHK(hipGetLastError());
         bool tail = false;
         std::vector<size_t> checks;  // event slots of status copies, with their copy index
@@ -880,25 +1054,41 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
             if (it > cap) return rtw_fail(RTW_ERR_HIP, "wavefront did not drain (internal error)");
             {
                 size_t e0 = 0, e1 = 0;
+                if (fused) {
+                    if (timed) {
+                        e0 = ev++, e1 = ev++;
+                        if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
+                        HIPCHK(hipEventRecord(h->events[e0], st));
+                    }
+                    launch_segment(false, h->features, h->shade_mask, grid, st, h->S, J, A, FR, C, h->scene_base,
+                                   h->shade_bytes);
+                    if (timed) {
+                        HIPCHK(hipEventRecord(h->events[e1], st));
+                        isect_ev.push_back({e0, e1});
+                    }
+                } else {
                 if (timed) {
                     e0 = ev++, e1 = ev++;
                     if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
                     HIPCHK(hipEventRecord(h->events[e0], st));
                 }
-                launch_intersect(h->features, grid, st, h->S, A, ht, hid, C);
+                launch_intersect(h->features, grid, st, h->S, A, FR, ht, hid, C);
                 if (timed) {
                     HIPCHK(hipEventRecord(h->events[e1], st));
                     isect_ev.push_back({e0, e1});
+                }
+                if (timed_shade) {
                     e0 = ev++, e1 = ev++;
                     if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
                     HIPCHK(hipEventRecord(h->events[e0], st));
                 }
-                launch_shade(h->shade_mask, grid, st, h->S, J, A, ht, hid, C, h->scene_base, h->shade_bytes);
-                if (timed) {
+                launch_shade(h->shade_mask, grid, st, h->S, J, A, FR, ht, hid, C, h->scene_base, h->shade_bytes);
+                if (timed_shade) {
                     HIPCHK(hipEventRecord(h->events[e1], st));
                     shade_ev.push_back({e0, e1});
                 }
-                if (!tail) hipLaunchKernelGGL(k_regen, dim3(regen_grid), dim3(kBlock), 0, st, J, A, C);
+                }
+                if (!tail) hipLaunchKernelGGL(k_regen, dim3(regen_grid), dim3(kBlock), 0, st, J, A, FR, C);
                 HIPCHK(hipGetLastError());
                 stats.launches_intersect++;
                 stats.iterations++;
@@ -926,7 +1116,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
             }
         }
         hipLaunchKernelGGL(k_reduce, dim3(std::min<uint64_t>((npix + kBlock - 1) / kBlock, 4096)), dim3(kBlock), 0, st,
-                           J.Lr, J.Lg, J.Lb, (uint32_t)npix, S_pass, run);
+                           J.L, (uint32_t)npix, S_pass, run);
         HIPCHK(hipGetLastError());
         stats.samples += J.total;
     }
@@ -950,7 +1140,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, ev_begin, ev_end));
     stats.ms_total = ms;
-    stats.segments = h->host_ctrs[63].segments;
+    for (int k = 0; k < 8; ++k) stats.segments += h->host_ctrs[63].segments[k].v;
     for (auto& p : isect_ev) {
         HIPCHK(hipEventElapsedTime(&ms, h->events[p.first], h->events[p.second]));
         stats.ms_intersect += ms;

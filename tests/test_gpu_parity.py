@@ -129,3 +129,21 @@ def test_reference_default_config_matches_committed_render(gpu):
     rms = float(np.sqrt(((blocks - np.array(g["block16_mean"])) ** 2).mean()))
     assert np.all(np.abs(dmean) < 1.5), dmean
     assert rms < 2.5, rms
+
+
+@pytest.mark.parametrize("scene,bvh", [("cornell_box", False), ("random_balls", True), ("dielectric", False)])
+def test_split_and_fused_kernels_agree(gpu, monkeypatch, scene, bvh):
+    """The fused traversal+shading kernel (k_segment) and the split pair
+    (k_intersect, k_shade; RTW_SPLIT=1) run the same arithmetic in the same
+    order: bit-identical accumulators and segment counts."""
+    nx, ny, spp, depth = 40, 30, 4, 50
+    sd = gpu.SceneDesc(scene, nx / ny, use_bvh=bvh)
+    ds = gpu.DeviceScene(sd)
+    try:
+        a, sa = ds.render_accumulate(nx, ny, spp, depth, seed=5)
+        monkeypatch.setenv("RTW_SPLIT", "1")
+        b, sb = ds.render_accumulate(nx, ny, spp, depth, seed=5)
+    finally:
+        ds.close()
+    assert sa["segments"] == sb["segments"]
+    assert np.array_equal(a, b)
