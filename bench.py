@@ -33,7 +33,11 @@ sys.path.insert(0, str(ROOT))
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"] if (ROOT / "BASELINE.json").exists() else \
     "Msamples/s (rays traced/s) at fixed W×H×spp×max_depth; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-ALGO_BYTES_PER_SEGMENT = 68  # traversal: read ray o,d,time (56 B), write hit t + id (12 B)
+# Algorithmic bytes of the roofline kernel come from the library
+# (rtw_stats.bytes_intersect = 68 B per traversal: ray 56 B in, hit 12 B out,
+# SURVEY.md 8(d)).  The default kernel, k_persist, fuses traversal and
+# shading and keeps the path in registers, so these bytes never actually
+# reach HBM: the kernel is fp64-VALU / latency bound.
 
 
 def parse():
@@ -96,7 +100,7 @@ def main():
     import torch
     import torch.distributed as dist
     from raytracingweekend_amd import build
-    from raytracingweekend_amd.render import DeviceScene, SceneDesc, finalize, write_ppm
+    from raytracingweekend_amd.render import DeviceScene, SceneDesc, write_ppm
 
     if not (ROOT / "raytracingweekend_amd" / "librtw.so").exists():
         build.build_library()
@@ -110,18 +114,21 @@ def main():
     sd = SceneDesc(args.scene, nx / ny, args.bvh)
     ds = DeviceScene(sd, local_rank)
     accum = torch.zeros(nx * ny * 3, dtype=torch.float64, device=dev)
+    canvas = torch.zeros_like(accum)
     collect = not args.no_kernel_times
 
     def step(timed: bool):
+        # one render of the workload: radiance sums on every rank, reduced to
+        # rank 0, finalised to the canvas there (RayTracingWeekend.cpp:211-250);
+        # the canvas stays in HBM like the inputs
         accum.zero_()
         _, st = ds.render_accumulate(nx, ny, total_spp, depth, args.seed, spp_begin=rank * spp, spp_count=spp,
                                      accum=accum, collect_kernel_times=collect and timed,
                                      wavefront_paths=args.paths)
         if world > 1:
             dist.reduce(accum, dst=0)
-        canvas = None
         if rank == 0:
-            canvas = finalize(accum.cpu().numpy(), nx, ny, total_spp)
+            ds.finalize_device(accum, nx, ny, total_spp, canvas)
         return st, canvas
 
     for _ in range(args.warmup):
@@ -148,18 +155,22 @@ def main():
     seg = sum(s["segments"] for s in stats)
     ms_isect = sum(s["ms_intersect"] for s in stats)
     launches = sum(s["launches_intersect"] for s in stats)
+    algo = sum(s["bytes_intersect"] for s in stats)
+    mode = os.environ.get("RTW_MODE", "persistent")
+    kernel = ("k_intersect" if os.environ.get("RTW_SPLIT") == "1" else "k_segment") if mode == "wavefront" \
+        else "k_persist"
     if world > 1:
-        v = torch.tensor([seg, ms_isect, launches], dtype=torch.float64, device=dev)
+        v = torch.tensor([seg, ms_isect, launches, algo], dtype=torch.float64, device=dev)
         dist.all_reduce(v)
-        seg_all, ms_all, launches_all = float(v[0]), float(v[1]), float(v[2])
+        seg_all, ms_all, launches_all, algo_all = float(v[0]), float(v[1]), float(v[2]), float(v[3])
     else:
-        seg_all, ms_all, launches_all = float(seg), ms_isect, float(launches)
+        seg_all, ms_all, launches_all, algo_all = float(seg), ms_isect, float(launches), algo
 
     if rank == 0:
         value = samples_per_step * args.steps / elapsed / 1e6
         roofline = None
         if collect and ms_all > 0:
-            achieved = ALGO_BYTES_PER_SEGMENT * seg_all / (ms_all * 1e-3) / 1e9
+            achieved = algo_all / (ms_all * 1e-3) / 1e9
             traffic = None
             pmc = ROOT / "profiles" / "pmc_intersect.json"
             if pmc.exists():
@@ -169,10 +180,10 @@ def main():
                     traffic = None
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "kernel": "k_intersect", "launches": int(launches_all),
+                        "kernel": kernel, "launches": int(launches_all),
                         "avg_launch_ms": round(ms_all / max(launches_all, 1), 4),
-                        "algo_bytes_per_launch": round(ALGO_BYTES_PER_SEGMENT * seg_all / max(launches_all, 1), 1),
-                        "bytes_per_segment": ALGO_BYTES_PER_SEGMENT}
+                        "algo_bytes_per_launch": round(algo_all / max(launches_all, 1), 1),
+                        "bytes_per_segment": round(algo_all / max(seg_all, 1), 2)}
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -185,6 +196,7 @@ def main():
                        "bvh": args.bvh, "parallelism": f"spp-shard x{world} + RCCL reduce"},
             "msegments_per_s": round(seg_all / args.steps / (elapsed / args.steps) / 1e6, 2) if seg_all else None,
             "segments_per_sample": round(seg_all / (samples_per_step * args.steps), 4),
+            "ms_render_gpu": round(sum(s["ms_total"] for s in stats) / len(stats), 3),
             "roofline": roofline,
             "cpu_baseline": None,
         }
@@ -194,8 +206,8 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(args, threads)
             except Exception as e:  # reported, never fatal for the GPU number
                 out["cpu_baseline"] = {"error": repr(e)}
-        if args.ppm and canvas is not None:
-            write_ppm(args.ppm, canvas, nx, ny)
+        if args.ppm:
+            write_ppm(args.ppm, canvas.cpu().numpy(), nx, ny)
         print(json.dumps(out), flush=True)
     ds.close()
     if world > 1:

@@ -226,13 +226,16 @@ typedef struct rtw_render_params {
 typedef struct rtw_stats {
     uint64_t samples;        /* camera samples completed                          */
     uint64_t segments;       /* ray traversals (world hit queries), device-counted */
-    uint64_t iterations;     /* wavefront iterations (intersect+shade pairs)     */
-    uint64_t launches_intersect;
+    uint64_t iterations;     /* wavefront iterations                              */
+    uint64_t launches_intersect; /* traversal launches: k_persist (default: one
+                                    per pass), k_segment (wavefront, fused
+                                    traversal + shading) or k_intersect (split) */
     double ms_total;         /* wall time of the call (hipEvents, whole stream)   */
-    double ms_intersect;     /* sum of intersect-kernel durations (if collected)  */
-    double ms_shade;         /* sum of shade/regenerate-kernel durations          */
-    double ms_finalize;      /* per-pixel ordered reduction                       */
-    double bytes_intersect;  /* algorithmic bytes moved by intersect kernels      */
+    double ms_intersect;     /* sum of those launches' durations (if collected)   */
+    double ms_shade;         /* sum of k_shade durations (split pair, level 2)    */
+    double ms_finalize;      /* per-pixel ordered reduction (not collected)       */
+    double bytes_intersect;  /* algorithmic traversal bytes: 68 per segment (ray
+                                56 B in, hit 12 B out)             */
 } rtw_stats;
 
 /* Number of visible HIP devices (0 if none). */
@@ -250,6 +253,11 @@ int rtw_render_accumulate(void* scene_handle, const rtw_camera_desc* camera,
 
 /* canvas = min(sqrt(accum / spp), 1) per channel (RayTracingWeekend.cpp:241-244). */
 void rtw_finalize_canvas(const double* accum_rgb, int nx, int ny, int spp, double* canvas_rgb);
+
+/* The same on the GPU, for device buffers of the handle's device (stream
+ * ordered after the handle's renders; returns when the canvas is written). */
+int rtw_finalize_canvas_device(void* scene_handle, const double* accum_rgb_dev, int nx, int ny, int spp,
+                               double* canvas_rgb_dev);
 
 /* P3 PPM, rows ny-1..0, int(255.99f * c) (RayTracingWeekend.cpp:252-276). */
 int rtw_write_ppm(const char* path, const double* canvas_rgb, int nx, int ny);

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -98,6 +99,7 @@ SIGNATURES = {
                                         C.c_void_p, C.POINTER(rtw_stats)]),
     "rtw_finalize_canvas": (None, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "rtw_write_ppm": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
+    "rtw_finalize_canvas_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "rtw_scene_free": (None, [C.c_void_p]),
     "rtw_last_error": (C.c_char_p, []),
     "rtw_path_seed": (C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint32]),
@@ -113,6 +115,14 @@ def lib():
     """Load librtw.so (once).  Raises if the native library is missing."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7
+        # (same soname as /opt/rocm's), and torch's GPU init fails if the
+        # system runtime was loaded first -- so let torch load it first.
+        if os.environ.get("RTW_NO_TORCH") != "1" and "torch" not in sys.modules:
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         if not LIB_PATH.exists():
             raise RuntimeError(f"native library {LIB_PATH} is missing: build it with "
                                f"`python -m raytracingweekend_amd.build` (there is no CPU fallback)")

@@ -52,13 +52,13 @@ def _run(cmd):
     return r
 
 
-def _compile(src: Path, force: bool) -> Path:
-    obj = BUILD / (src.name + ".o")
+def _compile(src: Path, force: bool, extra=(), tag: str = "") -> Path:
+    obj = BUILD / (src.name + tag + ".o")
     if force or _newer(obj, [src, *HEADERS, Path(__file__)]):
         if src.suffix == ".hip":
-            cmd = [HIPCC, *DEVICE, *COMMON, *INCLUDES, "-x", "hip", "-c", str(src), "-o", str(obj)]
+            cmd = [HIPCC, *DEVICE, *COMMON, *extra, *INCLUDES, "-x", "hip", "-c", str(src), "-o", str(obj)]
         else:
-            cmd = [HIPCC, *COMMON, *INCLUDES, "-c", str(src), "-o", str(obj)]
+            cmd = [HIPCC, *COMMON, *extra, *INCLUDES, "-c", str(src), "-o", str(obj)]
         _run(cmd)
     return obj
 
@@ -71,6 +71,31 @@ def build_library(force: bool = False) -> Path:
     if force or _newer(LIB, objs):
         _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)])
     return LIB
+
+
+def build_variant_library(name: str, defines, force: bool = False) -> Path:
+    """_build/librtw_<name>.so: the library with extra -D flags on the kernels
+    (tuning experiments; select with RTW_LIBRARY=...)."""
+    BUILD.mkdir(exist_ok=True)
+    out = BUILD / f"librtw_{name}.so"
+    objs = [_compile(s, force, [f"-D{d}" for d in defines], f".{name}") for s in DEVICE_SOURCES]
+    objs += [_compile(s, force) for s in HOST_SOURCES]
+    if force or _newer(out, objs):
+        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), "-o", str(out)])
+    return out
+
+
+def build_profiling_library(force: bool = False) -> Path:
+    """_build/librtw_prof.so: the same library with the kernels' section
+    profiler compiled in (-DRTW_PROF); select it with RTW_LIBRARY=... .
+    A measurement tool only: its timers perturb the kernels."""
+    BUILD.mkdir(exist_ok=True)
+    out = BUILD / "librtw_prof.so"
+    objs = [_compile(s, force, ["-DRTW_PROF"], ".prof") for s in DEVICE_SOURCES]
+    objs += [_compile(s, force) for s in HOST_SOURCES]
+    if force or _newer(out, objs):
+        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), "-o", str(out)])
+    return out
 
 
 def build_cli(force: bool = False) -> Path:

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "rtw_gpu.h"
+#include "rtw_div.h"
 
 #define RTW_D __device__ __forceinline__
 
@@ -27,6 +28,7 @@ constexpr double kOneMinusUlp = 0.99999999999999989; // nextafter(1.0, 0.0)
 // generate_canonical's divisor: (double)((long double)R * R), R = 2^31 - 2
 constexpr double kCanonDiv = 4611686009837453312.0;
 constexpr double kCanonR = 2147483646.0;
+constexpr double kCanonRcp = 1.0 / kCanonDiv;  // RN(1/x): constant folding is IEEE
 
 // ------------------------------------------------------------------ vec3
 struct d3 {
@@ -70,7 +72,7 @@ RTW_D double canon(uint32_t& s) {
     const double e2 = (double)(mr_next(s) - 1u);
     double sum = 0.0 + e1 * 1.0;
     sum = sum + e2 * kCanonR;
-    double r = sum / kCanonDiv;
+    double r = div_rcp(sum, kCanonDiv, kCanonRcp);  // sum in [0, 2^62]: always in the guard
     return r >= 1.0 ? kOneMinusUlp : r;
 }
 RTW_D double rnd01(uint32_t& s) { return canon(s) * (1.0 - 0.0) + 0.0; }
@@ -111,17 +113,6 @@ RTW_D d3 random_cosine_direction(uint32_t& s) {  // utility.h:54-67
     const double z = __builtin_sqrt(1 - r2);
     const double phi = kTwoPi * r1;
     const double sq = __builtin_sqrt(r2);
-    double sp, cp;
-    sincos(phi, &sp, &cp);
-    return d3{cp * sq, sp * sq, z};
-}
-
-RTW_D d3 random_to_sphere(uint32_t& s, double radius, double dist2) {  // utility.h:69-81
-    const double r1 = rnd01(s);
-    const double r2 = rnd01(s);
-    const double z = 1 + r2 * (__builtin_sqrt(1 - radius * radius / dist2) - 1);
-    const double phi = kTwoPi * r1;
-    const double sq = __builtin_sqrt(1 - z * z);
     double sp, cp;
     sincos(phi, &sp, &cp);
     return d3{cp * sq, sp * sq, z};
@@ -617,21 +608,45 @@ RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
     return 0.0;  // hittable.h:36
 }
 
-RTW_D d3 light_random(const scene& S, const rtw_light& L, d3 o, uint32_t& rng) {
-    if (L.kind == RTW_LIGHT_XZ_RECT) {  // hittable.h:224-228, z drawn first
+// mixture_pdf(cosine_pdf(n), hittable_pdf(lights, o))::generate (pdf.h:55-79)
+// as one code path: the cosine lobe (utility.h:54-67) and a sphere light
+// (sphere.h:101-108, utility.h:69-81) share their sqrt / sincos / onb tail,
+// so a wave whose lanes took different branches pays for one sincos, not
+// two.  Every lane draws and rounds exactly as its own branch would.
+RTW_D d3 mixture_generate(const scene& S, const onb& uvw, d3 o, uint32_t& rng) {
+    const bool cosine = rnd01(rng) < 0.5;
+    rtw_light L{RTW_LIGHT_DEFAULT, 0};
+    int kind = -1;  // the cosine lobe
+    if (!cosine) {
+        L = S.lights[random_int(rng, 0, S.n_lights - 1)];
+        kind = L.kind;
+    }
+    if (kind == RTW_LIGHT_DEFAULT) return d3{1, 0, 0};  // hittable.h:37
+    const double r1 = rnd01(rng);
+    const double r2 = rnd01(rng);
+    if (kind == RTW_LIGHT_XZ_RECT) {  // hittable.h:224-228, z drawn first
         const rtw_prim& q = S.prims[L.prim];
-        const double rz = rnd(rng, q.p[2], q.p[3]);
-        const double rx = rnd(rng, q.p[0], q.p[1]);
+        const double rz = q.p[2] + (q.p[3] - q.p[2]) * r1;
+        const double rx = q.p[0] + (q.p[1] - q.p[0]) * r2;
         return d3{rx, q.p[4], rz} - o;
     }
-    if (L.kind == RTW_LIGHT_SPHERE) {  // sphere.h:101-108
+    const bool sph = kind == RTW_LIGHT_SPHERE;
+    onb basis = uvw;
+    double a1 = 1 - r2;
+    if (sph) {
         const rtw_prim& q = S.prims[L.prim];
         const d3 direction = ld3(q.p) - o;
         const double distance_squared = len2(direction);
-        const onb uvw = onb_from_w(direction);
-        return local(uvw, random_to_sphere(rng, q.p[3], distance_squared));
+        basis = onb_from_w(direction);
+        a1 = 1 - q.p[3] * q.p[3] / distance_squared;
     }
-    return d3{1, 0, 0};  // hittable.h:37
+    const double s1 = __builtin_sqrt(a1);
+    const double z = sph ? 1 + r2 * (s1 - 1) : s1;
+    const double sq = __builtin_sqrt(sph ? 1 - z * z : r2);
+    const double phi = kTwoPi * r1;
+    double sp, cp;
+    sincos(phi, &sp, &cp);
+    return local(basis, d3{cp * sq, sp * sq, z});
 }
 
 RTW_D double lights_pdf_value(const scene& S, d3 o, d3 v) {  // hittable_list.h:44-53

@@ -111,13 +111,18 @@ __device__ __forceinline__ void sample_coords(const job_t& J, uint32_t q, int& i
 
 // Render-loop body RayTracingWeekend.cpp:227-231 for sample q: jitter,
 // camera::get_ray -> staging entry k.
-__device__ __forceinline__ void raygen(const job_t& J, const fresh_t& F, uint32_t k, uint32_t q) {
+__device__ __forceinline__ ray camera_sample(const job_t& J, uint32_t q, uint32_t& rng) {
     int i, j, s;
     sample_coords(J, q, i, j, s);
-    uint32_t rng = path_seed(J.seed_mix, (uint32_t)(j * J.nx + i), (uint32_t)s);
+    rng = path_seed(J.seed_mix, (uint32_t)(j * J.nx + i), (uint32_t)s);
     const double u = (double)(i + rnd01(rng)) / (double)J.nx;
     const double v = (double)(j + rnd01(rng)) / (double)J.ny;
-    const ray r = camera_ray(J.cam, u, v, rng);
+    return camera_ray(J.cam, u, v, rng);
+}
+
+__device__ __forceinline__ void raygen(const job_t& J, const fresh_t& F, uint32_t k, uint32_t q) {
+    uint32_t rng;
+    const ray r = camera_sample(J, q, rng);
     F.ox[k] = r.o.x, F.oy[k] = r.o.y, F.oz[k] = r.o.z;
     F.dx[k] = r.d.x, F.dy[k] = r.d.y, F.dz[k] = r.d.z;
     F.tm[k] = r.t;
@@ -226,6 +231,38 @@ __global__ __launch_bounds__(kBlock) void k_intersect(scene S, paths_t P, fresh_
     }
 }
 
+// Section profiler (profiling builds only: -DRTW_PROF).  Each lane charges
+// the clock since its previous mark to the section it just finished; the
+// per-lane sums land in g_prof and rtw_render_accumulate prints them.
+enum { PS_LOOP, PS_LOAD, PS_TRAVERSE, PS_HIT, PS_SAMPLE, PS_PDF, PS_STORE, PS_N };
+#ifdef RTW_PROF
+__device__ unsigned long long g_prof[PS_N];
+struct prof_t {
+    uint64_t t;
+    uint64_t acc[PS_N];
+    __device__ prof_t() : t(clock64()) {
+        for (int k = 0; k < PS_N; ++k) acc[k] = 0;
+    }
+    __device__ __forceinline__ void mark(int k) {
+        const uint64_t now = clock64();
+        acc[k] += now - t;
+        t = now;
+    }
+    __device__ void flush() {
+        for (int k = 0; k < PS_N; ++k) {
+            unsigned long long v = acc[k];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+            if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof[k], v);
+        }
+    }
+};
+#else
+struct prof_t {
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush() {}
+};
+#endif
+
 // Background of RayTracingWeekend.cpp:141-159.
 __device__ __forceinline__ d3 background(const scene& S, const d3& dir) {
     if (S.background != RTW_BG_GRADIENT) return d3{0, 0, 0};
@@ -234,19 +271,26 @@ __device__ __forceinline__ d3 background(const scene& S, const d3& dir) {
     return d3{1.0, 1.0, 1.0} * (1.0 - t) + d3{0.5f, 0.7f, 1.0} * t;  // lerp, vec3.h:84-87
 }
 
-// One segment of color() (RayTracingWeekend.cpp:52-159) for the path x in
-// pool slot i, whose world hit is (t, prim) and whose engine state is rng.
-// Returns true when the path ends (radiance in L); otherwise the scattered
-// ray, throughput, rng and depth are written to the slot (which stops being
-// fresh).
+// A path between two color() calls: the ray of the next call, the product
+// of the attenuation / pdf factors so far, its engine, the depth argument of
+// the next call and its sample id.
+struct path_st {
+    ray r;
+    d3 thr;
+    uint32_t rng, depth, q;
+};
+
+// One segment of color() (RayTracingWeekend.cpp:52-159) for path x whose
+// world hit is (t, prim).  Returns true when the path ends (its radiance in
+// L); otherwise x becomes the scattered path.  The recursion's inside-out
+// products are folded forward: L = thr * (last emitted / background), with
+// the reference's per-bounce factor attenuation * scattering_pdf / pdf.
 template <int M>
-__device__ __forceinline__ bool shade_one(const scene& S, const job_t& J, const paths_t& P, const fresh_t& FR,
-                                          uint32_t i, const path_in& x, uint32_t rng, double t, int32_t prim, d3& L,
-                                          uint32_t& q) {
-    const uint32_t dw = x.depth;
-    const ray& r = x.r;
-    const d3 thr = x.fresh ? d3{1.0, 1.0, 1.0} : d3{P.tr[i], P.tg[i], P.tb[i]};
-    q = x.fresh ? FR.qid[x.src] : P.qid[i];
+__device__ __forceinline__ bool shade_core(const scene& S, path_st& x, double t, int32_t prim, d3& L, prof_t& pf) {
+    const ray r = x.r;
+    const d3 thr = x.thr;
+    uint32_t rng = x.rng;
+    const uint32_t depth = x.depth;
     if (prim == -1) {
         L = thr * background(S, r.d);
         return true;
@@ -259,7 +303,7 @@ __device__ __forceinline__ bool shade_one(const scene& S, const job_t& J, const 
         return true;
     }
     const rtw_material& m = S.materials[mat];
-    const uint32_t depth = x.fresh ? (uint32_t)J.max_depth : dw;
+    pf.mark(PS_HIT);
     d3 dir;
     d3 f;  // throughput factor of this bounce
     if (m.type == RTW_MAT_DIFFUSE_LIGHT) {  // material.h:232-244: no scatter
@@ -294,14 +338,11 @@ __device__ __forceinline__ bool shade_one(const scene& S, const job_t& J, const 
     } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
         const d3 att = texture_value<M>(S, m.texture, p);
         const onb uvw = onb_from_w(n);
+        pf.mark(PS_HIT);
         double pdf_val;
         if (S.n_lights > 0) {  // mixture_pdf(cosine_pdf, hittable_pdf(lights)) pdf.h:55-79
-            if (rnd01(rng) < 0.5) {
-                dir = local(uvw, random_cosine_direction(rng));
-            } else {
-                const int k = random_int(rng, 0, S.n_lights - 1);
-                dir = light_random(S, S.lights[k], p, rng);
-            }
+            dir = mixture_generate(S, uvw, p, rng);
+            pf.mark(PS_SAMPLE);
             const double cw = dot(normalize(dir), uvw.w);
             const double p0 = (cw <= 0) ? 0 : cw / kPi;
             pdf_val = 0.5 * p0 + 0.5 * lights_pdf_value(S, p, dir);
@@ -317,19 +358,40 @@ __device__ __forceinline__ bool shade_one(const scene& S, const job_t& J, const 
         const double cosine = dot(n, normalize(dir));  // material.h:115-119
         const double spdf = cosine < 0 ? 0 : cosine / kPi;
         f = (att * spdf) / pdf_val;
+        pf.mark(PS_PDF);
     }
     if (depth <= 1) {  // the next color() call has depth 0 and returns 0
         L = d3{0, 0, 0};
         return true;
     }
-    const d3 nt = thr * f;
-    P.ox[i] = p.x, P.oy[i] = p.y, P.oz[i] = p.z;
-    P.dx[i] = dir.x, P.dy[i] = dir.y, P.dz[i] = dir.z;
-    P.tm[i] = r.t;
-    P.tr[i] = nt.x, P.tg[i] = nt.y, P.tb[i] = nt.z;
-    P.rng[i] = rng;
-    P.depth[i] = depth - 1;
-    P.qid[i] = q;
+    x.r = ray{p, dir, r.t};
+    x.thr = thr * f;
+    x.rng = rng;
+    x.depth = depth - 1;
+    return false;
+}
+
+// The wavefront form: path x (read from pool slot i or, fresh, from staging)
+// -> shade_core -> continuation written back to slot i (no longer fresh).
+template <int M>
+__device__ __forceinline__ bool shade_one(const scene& S, const job_t& J, const paths_t& P, const fresh_t& FR,
+                                          uint32_t i, const path_in& x, uint32_t rng, double t, int32_t prim, d3& L,
+                                          uint32_t& q, prof_t& pf) {
+    path_st s;
+    s.r = x.r;
+    s.thr = x.fresh ? d3{1.0, 1.0, 1.0} : d3{P.tr[i], P.tg[i], P.tb[i]};
+    s.rng = rng;
+    s.depth = x.fresh ? (uint32_t)J.max_depth : x.depth;
+    s.q = x.fresh ? FR.qid[x.src] : P.qid[i];
+    q = s.q;
+    if (shade_core<M>(S, s, t, prim, L, pf)) return true;
+    P.ox[i] = s.r.o.x, P.oy[i] = s.r.o.y, P.oz[i] = s.r.o.z;
+    P.dx[i] = s.r.d.x, P.dy[i] = s.r.d.y, P.dz[i] = s.r.d.z;
+    P.tm[i] = s.r.t;
+    P.tr[i] = s.thr.x, P.tg[i] = s.thr.y, P.tb[i] = s.thr.z;
+    P.rng[i] = s.rng;
+    P.depth[i] = s.depth;
+    P.qid[i] = s.q;
     return false;
 }
 
@@ -373,7 +435,8 @@ __global__ __launch_bounds__(kBlock) void k_shade(scene S, job_t J, paths_t P, f
         uint32_t q;
         const path_in x = load_ray(P, FR, i, dw);
         const uint32_t rng = x.fresh ? FR.rng[x.src] : P.rng[i];
-        if (shade_one<M>(SS, J, P, FR, i, x, rng, ht[i], hid[i], L, q)) {
+        prof_t pf;
+        if (shade_one<M>(SS, J, P, FR, i, x, rng, ht[i], hid[i], L, q, pf)) {
             double* o = J.L + 3 * (size_t)q;
             o[0] = L.x, o[1] = L.y, o[2] = L.z;
             P.depth[i] = 0;
@@ -384,8 +447,13 @@ __global__ __launch_bounds__(kBlock) void k_shade(scene S, job_t J, paths_t P, f
 // Fused segment: traversal + shading of each live path in one pass over the
 // pool (the ray is read once; no hit records go through HBM).  Same results
 // as k_intersect followed by k_shade.
+#ifdef RTW_SEG_WAVES  // occupancy experiments: cap registers for N waves per SIMD
+#define RTW_SEG_ATTR __attribute__((amdgpu_waves_per_eu(RTW_SEG_WAVES)))
+#else
+#define RTW_SEG_ATTR
+#endif
 template <int F, int M, bool LDS>
-__global__ __launch_bounds__(kBlock) void k_segment(scene S, job_t J, paths_t P, fresh_t FR, ctrs_t* C,
+__global__ __launch_bounds__(kBlock) RTW_SEG_ATTR void k_segment(scene S, job_t J, paths_t P, fresh_t FR, ctrs_t* C,
                                                     const char* base, uint32_t bytes) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kWaves];
@@ -398,23 +466,117 @@ __global__ __launch_bounds__(kBlock) void k_segment(scene S, job_t J, paths_t P,
     const scene SS = LDS ? lds_scene(S, base, s_scene) : S;
     const uint32_t n = C->n;
     uint32_t live = 0;
+    prof_t pf;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         const uint32_t dw = P.depth[i];
         if (dw == 0) continue;
+        pf.mark(PS_LOOP);
         const path_in x = load_ray(P, FR, i, dw);
         uint32_t rng = x.fresh ? FR.rng[x.src] : P.rng[i];
+        pf.mark(PS_LOAD);
         const hit_state h = world_closest<F>(S, x.r, rng);
+        pf.mark(PS_TRAVERSE);
         ++live;
         d3 L;
         uint32_t q;
-        if (shade_one<M>(SS, J, P, FR, i, x, rng, h.t, h.prim, L, q)) {
+        if (shade_one<M>(SS, J, P, FR, i, x, rng, h.t, h.prim, L, q, pf)) {
             double* o = J.L + 3 * (size_t)q;
             o[0] = L.x, o[1] = L.y, o[2] = L.z;
             P.depth[i] = 0;
         }
+        pf.mark(PS_STORE);
     }
+    pf.flush();
     for (int off = 32; off > 0; off >>= 1) live += __shfl_down(live, off, 64);
     if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = live;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int k = 0; k < kWaves; ++k) t += s_cnt[k];
+        if (t) atomicAdd(&C->segments[blockIdx.x % 8].v, t);
+    }
+}
+
+// Persistent form: every lane keeps its path in registers and runs it to the
+// end, then takes the next sample from the sharded queue -- one launch per
+// pass, no path state through HBM, no regeneration or compaction launches.
+// A wave refills its idle lanes with ONE atomic (lane 0 reserves as many
+// consecutive ids of its shard as lanes are idle; neighbouring ids are
+// neighbouring pixels), stealing from the other shards once its own is dry;
+// it exits when the queue is exhausted and its last path has ended.
+template <int F, int M, bool LDS>
+__global__ __launch_bounds__(kBlock) RTW_SEG_ATTR void k_persist(scene S, job_t J, ctrs_t* C, const char* base,
+                                                                 uint32_t bytes) {
+    extern __shared__ __attribute__((aligned(16))) char s_scene[];
+    __shared__ uint32_t s_cnt[kWaves];
+    if (LDS) {
+        const uint4* src = reinterpret_cast<const uint4*>(base);
+        uint4* dst = reinterpret_cast<uint4*>(s_scene);
+        for (uint32_t k = threadIdx.x; k < bytes / 16; k += kBlock) dst[k] = src[k];
+        __syncthreads();
+    }
+    const scene SS = LDS ? lds_scene(S, base, s_scene) : S;
+    const uint32_t lane = threadIdx.x & 63;
+    const int own = blockIdx.x % kQShards;
+    path_st x;
+    x.depth = 0;
+    bool open = true;  // wave-uniform: the queue may still hold samples
+    uint32_t segs = 0;
+    prof_t pf;
+    for (;;) {
+        const bool idle = x.depth == 0;
+        const unsigned long long m = __ballot(idle);
+        if (open && m) {
+            const uint32_t want = (uint32_t)__popcll(m);
+            const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+            uint32_t left = want, given = 0;
+            bool got = false;
+            uint32_t q = 0;
+            for (int a = 0; a < kQShards && left; ++a) {
+                const int sh = (own + a) % kQShards;
+                const unsigned long long lim = shard_limit(sh, J.total);
+                unsigned long long b = ~0ull;
+                if (lane == 0) {
+                    const bool dry = a > 0 && __hip_atomic_load(&C->qshard[sh].v, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT) >= lim;
+                    if (!dry) b = atomicAdd(&C->qshard[sh].v, (unsigned long long)left);
+                }
+                b = __shfl(b, 0, 64);
+                if (b == ~0ull || b >= lim) continue;
+                const uint32_t ok = (uint32_t)min((unsigned long long)left, lim - b);
+                if (idle && rank >= given && rank < given + ok) {
+                    q = (uint32_t)shard_sample(sh, b + (rank - given));
+                    got = true;
+                }
+                given += ok;
+                left -= ok;
+            }
+            if (left) open = false;
+            if (got) {
+                x.r = camera_sample(J, q, x.rng);
+                x.thr = d3{1.0, 1.0, 1.0};
+                x.depth = (uint32_t)J.max_depth;
+                x.q = q;
+            }
+        }
+        if (!__any(x.depth != 0)) break;
+        pf.mark(PS_LOAD);
+        if (x.depth != 0) {
+            const hit_state h = world_closest<F>(S, x.r, x.rng);
+            pf.mark(PS_TRAVERSE);
+            ++segs;
+            d3 L;
+            if (shade_core<M>(SS, x, h.t, h.prim, L, pf)) {
+                double* o = J.L + 3 * (size_t)x.q;
+                o[0] = L.x, o[1] = L.y, o[2] = L.z;
+                x.depth = 0;
+            }
+            pf.mark(PS_STORE);
+        }
+    }
+    pf.flush();
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_down(segs, off, 64);
+    if (lane == 0) s_cnt[threadIdx.x >> 6] = segs;
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
@@ -583,6 +745,15 @@ __global__ __launch_bounds__(kBlock) void k_emit(const double* __restrict__ run,
     }
 }
 
+// canvas = min(sqrt(accum / spp), 1) (RayTracingWeekend.cpp:241-244)
+__global__ __launch_bounds__(kBlock) void k_finalize(const double* __restrict__ accum, size_t n, double spp,
+                                                     double* __restrict__ canvas) {
+    for (size_t k = blockIdx.x * (size_t)kBlock + threadIdx.x; k < n; k += (size_t)gridDim.x * kBlock) {
+        const double s = __builtin_sqrt(accum[k] / spp);
+        canvas[k] = (1.0 < s) ? 1.0 : s;
+    }
+}
+
 // ======================================================================
 // host side
 // ======================================================================
@@ -639,6 +810,7 @@ struct handle_t {
     ctrs_t* host_ctrs = nullptr;  // pinned
     uint32_t pool_cap = 0;
     int grid = 2048;
+    int cus = 256;
     std::vector<hipEvent_t> events;
 };
 
@@ -784,6 +956,44 @@ bool launch_segment(bool probe, int f, int mask, int grid, hipStream_t st, const
     return false;
 }
 
+// Persistent kernel for the same instantiation set.  grid 0 = probe only.
+// The grid is the number of blocks that can be resident at once (occupancy
+// query per instantiation, cached), so every block starts immediately.
+template <int FF, int MM, bool LL>
+int persist_grid(size_t shm, int cus) {
+    static int blocks_per_cu = 0;
+    if (!blocks_per_cu) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_persist<FF, MM, LL>),
+                                                         kBlock, shm) != hipSuccess || nb <= 0)
+            nb = 2;
+        blocks_per_cu = nb;
+    }
+    return blocks_per_cu * cus;
+}
+
+bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C,
+                    const char* base, uint32_t bytes) {
+    const int pick = pick_shade_mask(mask);
+    const bool lds = bytes <= kShadeLdsMax;
+    const size_t shm = lds ? bytes : 0;
+#define RTW_PER(FF, MM, LL)                                                                                  \
+    if (f == (FF) && pick == (MM) && lds == (LL)) {                                                        \
+        if (!probe)                                                                                         \
+            hipLaunchKernelGGL((k_persist<FF, MM, LL>), dim3(persist_grid<FF, MM, LL>(shm, cus)), dim3(kBlock), shm, \
+                               st, S, J, C, base, bytes);                                                   \
+        return true;                                                                                       \
+    }
+    RTW_PER(0, SF_DIEL, true)
+    RTW_PER(0, SF_METAL | SF_DIEL, true)
+    RTW_PER(0, SF_ALL, true)
+    RTW_PER(0, SF_ALL, false)
+    RTW_PER(F_WBVH, SF_ALL, false)
+    RTW_PER(F_WBVH, SF_ALL, true)
+#undef RTW_PER
+    return false;
+}
+
 void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_t& J, const paths_t& A,
                   const fresh_t& F, const double* ht, const int32_t* hid, ctrs_t* C, const char* base, uint32_t bytes) {
     const int pick = pick_shade_mask(mask);
@@ -919,6 +1129,7 @@ extern "C" int rtw_scene_upload(int device, const rtw_scene_desc* desc, void** o
     handle_t* h = new handle_t;
     h->device = device;
     h->grid = prop.multiProcessorCount * 8;
+    h->cus = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return rtw_fail(RTW_ERR_HIP, "hipStreamCreate failed");
@@ -953,6 +1164,20 @@ extern "C" void rtw_scene_free(void* handle) {
     for (hipEvent_t e : h->events) hipEventDestroy(e);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
+}
+
+extern "C" int rtw_finalize_canvas_device(void* handle, const double* accum, int nx, int ny, int spp,
+                                          double* canvas) {
+    handle_t* h = static_cast<handle_t*>(handle);
+    if (!h || !accum || !canvas || nx <= 0 || ny <= 0 || spp <= 0)
+        return rtw_fail(RTW_ERR_INVALID, "rtw_finalize_canvas_device: bad argument");
+    HIPCHK(hipSetDevice(h->device));
+    const size_t n = (size_t)nx * (size_t)ny * 3;
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)std::min<size_t>((n + kBlock - 1) / kBlock, 8192)), dim3(kBlock), 0,
+                       h->stream, accum, n, (double)spp, canvas);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return RTW_OK;
 }
 
 extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera, const rtw_render_params* prm,
@@ -1035,12 +1260,40 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                        launch_segment(true, h->features, h->shade_mask, 0, st, h->S, J, A, FR, C, h->scene_base,
                                       h->shade_bytes);
     const int check_every = 4;
+    // execution form: persistent (paths in registers, one launch per pass)
+    // unless RTW_MODE=wavefront or no persistent instantiation covers the scene
+    const char* mode_env = std::getenv("RTW_MODE");
+    const bool persistent = !(mode_env && std::string(mode_env) == "wavefront") &&
+                            launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J, C, h->scene_base,
+                                           h->shade_bytes);
 
     for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
         J.total = (uint32_t)(S_pass * npix);
         J.s_begin = R.spp_begin + (int)done;
         const uint32_t n0 = std::min<uint32_t>(pool, J.total);
+        if (persistent) {
+            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kBlock), 0, st, A, C, 0u);  // reset the queue
+            size_t e0 = 0, e1 = 0;
+            if (timed) {
+                e0 = ev++, e1 = ev++;
+                if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
+                HIPCHK(hipEventRecord(h->events[e0], st));
+            }
+            launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base, h->shade_bytes);
+            HIPCHK(hipGetLastError());
+            if (timed) {
+                HIPCHK(hipEventRecord(h->events[e1], st));
+                isect_ev.push_back({e0, e1});
+            }
+            stats.launches_intersect++;
+            stats.iterations++;
+            hipLaunchKernelGGL(k_reduce, dim3(std::min<uint64_t>((npix + kBlock - 1) / kBlock, 4096)), dim3(kBlock), 0,
+                               st, J.L, (uint32_t)npix, S_pass, run);
+            HIPCHK(hipGetLastError());
+            stats.samples += J.total;
+            continue;
+        }
         hipLaunchKernelGGL(k_fill, dim3((n0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, A, C, n0);
         hipLaunchKernelGGL(k_regen, dim3(regen_grid), dim3(kBlock), 0, st, J, A, FR, C);
         HIPCHK(hipGetLastError());
@@ -1149,7 +1402,26 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         HIPCHK(hipEventElapsedTime(&ms, h->events[p.first], h->events[p.second]));
         stats.ms_shade += ms;
     }
-    stats.bytes_intersect = 68.0 * (double)stats.segments;  // 56 B ray in + 12 B hit out
+#ifdef RTW_PROF
+    {
+        unsigned long long pr[PS_N];
+        HIPCHK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prof), sizeof pr));
+        static const char* names[PS_N] = {"loop", "load", "traverse", "hit+material", "sample", "pdf", "store"};
+        double tot = 0;
+        for (int k = 0; k < PS_N; ++k) tot += (double)pr[k];
+        std::fprintf(stderr, "[rtw prof] lane-cycles per segment:");
+        for (int k = 0; k < PS_N; ++k)
+            std::fprintf(stderr, " %s %.0f (%.1f%%)", names[k], (double)pr[k] / std::max<double>(1, stats.segments),
+                         100.0 * pr[k] / std::max(1.0, tot));
+        std::fprintf(stderr, "\n");
+        std::memset(pr, 0, sizeof pr);
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof pr));
+    }
+#endif
+    // algorithmic traversal bytes: 56 B ray in +
+    // 12 B hit out per world query, whatever the execution form (k_persist
+    // keeps both in registers; k_segment / k_intersect stream them)
+    stats.bytes_intersect = 68.0 * (double)stats.segments;
     if (out_stats) *out_stats = stats;
     return RTW_OK;
 }

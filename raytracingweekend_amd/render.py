@@ -95,6 +95,20 @@ class DeviceScene:
               "rtw_render_accumulate")
         return accum, st.as_dict()
 
+    def finalize_device(self, accum, nx: int, ny: int, spp: int, canvas=None):
+        """canvas = min(sqrt(accum / spp), 1) on the GPU (torch float64 CUDA
+        tensors of nx*ny*3 on this device).  Returns the canvas tensor."""
+        import torch
+        if not (accum.is_cuda and accum.dtype == torch.float64 and accum.numel() == nx * ny * 3
+                and accum.is_contiguous()):
+            raise ValueError("accum must be a contiguous float64 CUDA tensor of nx*ny*3")
+        if canvas is None:
+            canvas = torch.empty_like(accum)
+        torch.cuda.synchronize(accum.device)
+        check(lib().rtw_finalize_canvas_device(self.handle, C.c_void_p(accum.data_ptr()), nx, ny, spp,
+                                               C.c_void_p(canvas.data_ptr())), "rtw_finalize_canvas_device")
+        return canvas
+
     def close(self):
         if self.handle:
             lib().rtw_scene_free(self.handle)

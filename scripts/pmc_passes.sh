@@ -1,0 +1,16 @@
+#!/bin/bash
+# Instruction-mix / stall / HBM-byte counters of a short bench run, one
+# rocprofv3 --pmc pass per counter group (kernel-trace only).
+# Usage: scripts/pmc_passes.sh <tag> [bench args...]
+set -e
+tag=$1; shift
+P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH"
+P2="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_WAVE_CYCLES"
+P3="SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS"
+P4="FETCH_SIZE GRBM_GUI_ACTIVE"
+P5="WRITE_SIZE GRBM_COUNT"
+i=1
+for grp in "$P1" "$P2" "$P3" "$P4" "$P5"; do
+    scripts/prof_pmc.sh "${tag}_$i" "$grp" "$@"
+    i=$((i+1))
+done

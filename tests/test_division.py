@@ -1,0 +1,18 @@
+"""rtw_div.h's Markstein division (used for generate_canonical's divide in
+every random draw on the device) is bit-identical to IEEE a / b: random,
+rounding-midpoint and edge operands (tests/cpp/div_check.cpp)."""
+import subprocess
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_markstein_division_is_ieee(tmp_path):
+    exe = tmp_path / "div_check"
+    # -mfma: hardware fma like the GPU's v_fma_f64 (glibc's fma is exact too)
+    subprocess.run(["g++", "-std=c++17", "-O2", "-mfma", "-ffp-contract=off",
+                    f"-I{ROOT / 'raytracingweekend_amd' / 'csrc'}", str(ROOT / "tests" / "cpp" / "div_check.cpp"),
+                    "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "2000000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout

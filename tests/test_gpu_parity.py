@@ -80,17 +80,21 @@ def test_sharding_is_exact(gpu):
         ds.close()
 
 
-def test_small_pool_and_passes(gpu, monkeypatch):
-    """A tiny path pool (heavy regeneration + tail compaction) and many passes
-    give the same canvas as the default configuration."""
+@pytest.mark.parametrize("mode", ["persistent", "wavefront"])
+def test_small_pool_and_passes(gpu, monkeypatch, mode):
+    """Many passes -- and, for the wavefront form, a tiny path pool (heavy
+    regeneration + tail compaction) -- give the same canvas as the default
+    configuration."""
     nx, ny, spp, depth = 24, 24, 5, 50
     sd = gpu.SceneDesc("cornell_box", 1.0)
     ds = gpu.DeviceScene(sd)
     try:
         a, _ = ds.render_accumulate(nx, ny, spp, depth, seed=11)
+        monkeypatch.setenv("RTW_MODE", mode)
         monkeypatch.setenv("RTW_PASS_SAMPLES", str(nx * ny * 2))
         b, st = ds.render_accumulate(nx, ny, spp, depth, seed=11, wavefront_paths=1000)
         assert np.array_equal(a, b)
+        assert st["iterations"] >= 3
     finally:
         ds.close()
 
@@ -132,18 +136,39 @@ def test_reference_default_config_matches_committed_render(gpu):
 
 
 @pytest.mark.parametrize("scene,bvh", [("cornell_box", False), ("random_balls", True), ("dielectric", False)])
-def test_split_and_fused_kernels_agree(gpu, monkeypatch, scene, bvh):
-    """The fused traversal+shading kernel (k_segment) and the split pair
-    (k_intersect, k_shade; RTW_SPLIT=1) run the same arithmetic in the same
-    order: bit-identical accumulators and segment counts."""
+def test_execution_forms_agree(gpu, monkeypatch, scene, bvh):
+    """The persistent kernel (k_persist, default), the wavefront's fused
+    traversal+shading kernel (k_segment; RTW_MODE=wavefront) and its split
+    pair (k_intersect, k_shade; + RTW_SPLIT=1) run the same arithmetic in the
+    same order per sample: bit-identical accumulators and segment counts."""
     nx, ny, spp, depth = 40, 30, 4, 50
     sd = gpu.SceneDesc(scene, nx / ny, use_bvh=bvh)
     ds = gpu.DeviceScene(sd)
     try:
         a, sa = ds.render_accumulate(nx, ny, spp, depth, seed=5)
-        monkeypatch.setenv("RTW_SPLIT", "1")
+        monkeypatch.setenv("RTW_MODE", "wavefront")
         b, sb = ds.render_accumulate(nx, ny, spp, depth, seed=5)
+        monkeypatch.setenv("RTW_SPLIT", "1")
+        c, sc = ds.render_accumulate(nx, ny, spp, depth, seed=5)
     finally:
         ds.close()
-    assert sa["segments"] == sb["segments"]
-    assert np.array_equal(a, b)
+    assert sa["segments"] == sb["segments"] == sc["segments"]
+    assert np.array_equal(a, b) and np.array_equal(a, c)
+
+
+def test_device_finalize_matches_host(gpu):
+    """rtw_finalize_canvas_device (the timed bench path) and the host
+    rtw_finalize_canvas give bit-identical canvases (IEEE sqrt and divide)."""
+    import torch
+    nx, ny, spp = 37, 23, 6
+    sd = gpu.SceneDesc("cornell_box", nx / ny)
+    ds = gpu.DeviceScene(sd)
+    try:
+        acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda:0")
+        ds.render_accumulate(nx, ny, spp, 50, seed=2, accum=acc)
+        acc[:3] = torch.tensor([0.0, 1e300, float(spp) * 4.0], dtype=torch.float64)  # clamp edges
+        dev = ds.finalize_device(acc, nx, ny, spp).cpu().numpy()
+    finally:
+        ds.close()
+    host = gpu.finalize(acc.cpu().numpy(), nx, ny, spp)
+    assert np.array_equal(dev, host)
