@@ -498,17 +498,27 @@ __global__ __launch_bounds__(kBlock) RTW_SEG_ATTR void k_segment(scene S, job_t 
 }
 
 // Persistent form: every lane keeps its path in registers and runs it to the
-// end, then takes the next sample from the sharded queue -- one launch per
-// pass, no path state through HBM, no regeneration or compaction launches.
-// A wave refills its idle lanes with ONE atomic (lane 0 reserves as many
-// consecutive ids of its shard as lanes are idle; neighbouring ids are
-// neighbouring pixels), stealing from the other shards once its own is dry;
-// it exits when the queue is exhausted and its last path has ended.
+// end, then takes the next camera sample -- one launch per pass, no path
+// state through HBM, no regeneration or compaction launches.
+//
+// Camera rays are made in batches of 64, one per lane (ray-gen never runs
+// for just the few lanes whose paths ended this iteration): a wave reserves
+// 64 consecutive sample ids of its queue shard with ONE atomic (neighbouring
+// ids are neighbouring pixels; other shards are stolen from once its own is
+// dry), every lane generates one ray into the wave's LDS buffer, and idle
+// lanes pop rays from that buffer.  A wave exits when the queue is exhausted,
+// its buffer is empty and its last path has ended.
+struct ray_batch {  // one wave's buffer of generated camera samples (LDS)
+    double ox[64], oy[64], oz[64], dx[64], dy[64], dz[64], tm[64];
+    uint32_t rng[64], q[64];
+};
+
 template <int F, int M, bool LDS>
 __global__ __launch_bounds__(kBlock) RTW_SEG_ATTR void k_persist(scene S, job_t J, ctrs_t* C, const char* base,
                                                                  uint32_t bytes) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kWaves];
+    __shared__ ray_batch s_batch[kWaves];
     if (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(base);
         uint4* dst = reinterpret_cast<uint4*>(s_scene);
@@ -517,47 +527,69 @@ __global__ __launch_bounds__(kBlock) RTW_SEG_ATTR void k_persist(scene S, job_t 
     }
     const scene SS = LDS ? lds_scene(S, base, s_scene) : S;
     const uint32_t lane = threadIdx.x & 63;
+    ray_batch& B = s_batch[threadIdx.x >> 6];
     const int own = blockIdx.x % kQShards;
     path_st x;
     x.depth = 0;
-    bool open = true;  // wave-uniform: the queue may still hold samples
+    bool open = true;      // wave-uniform: the queue may still hold samples
+    uint32_t bl = 0, bh = 0;  // wave-uniform: unread batch entries [bl, bh)
     uint32_t segs = 0;
     prof_t pf;
     for (;;) {
-        const bool idle = x.depth == 0;
-        const unsigned long long m = __ballot(idle);
-        if (open && m) {
-            const uint32_t want = (uint32_t)__popcll(m);
-            const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
-            uint32_t left = want, given = 0;
-            bool got = false;
-            uint32_t q = 0;
-            for (int a = 0; a < kQShards && left; ++a) {
-                const int sh = (own + a) % kQShards;
-                const unsigned long long lim = shard_limit(sh, J.total);
-                unsigned long long b = ~0ull;
-                if (lane == 0) {
-                    const bool dry = a > 0 && __hip_atomic_load(&C->qshard[sh].v, __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT) >= lim;
-                    if (!dry) b = atomicAdd(&C->qshard[sh].v, (unsigned long long)left);
+        for (int round = 0; round < 2; ++round) {
+            const unsigned long long m = __ballot(x.depth == 0);
+            if (!m) break;
+            if (bl == bh) {
+                if (!open) break;
+                // reserve up to 64 ids, own shard first
+                uint32_t left = 64, given = 0, q = 0;
+                bool got = false;
+                for (int a = 0; a < kQShards && left; ++a) {
+                    const int sh = (own + a) % kQShards;
+                    const unsigned long long lim = shard_limit(sh, J.total);
+                    unsigned long long b = ~0ull;
+                    if (lane == 0) {
+                        const bool dry = a > 0 && __hip_atomic_load(&C->qshard[sh].v, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT) >= lim;
+                        if (!dry) b = atomicAdd(&C->qshard[sh].v, (unsigned long long)left);
+                    }
+                    b = __shfl(b, 0, 64);
+                    if (b == ~0ull || b >= lim) continue;
+                    const uint32_t ok = (uint32_t)min((unsigned long long)left, lim - b);
+                    if (lane >= given && lane < given + ok) {
+                        q = (uint32_t)shard_sample(sh, b + (lane - given));
+                        got = true;
+                    }
+                    given += ok;
+                    left -= ok;
                 }
-                b = __shfl(b, 0, 64);
-                if (b == ~0ull || b >= lim) continue;
-                const uint32_t ok = (uint32_t)min((unsigned long long)left, lim - b);
-                if (idle && rank >= given && rank < given + ok) {
-                    q = (uint32_t)shard_sample(sh, b + (rank - given));
-                    got = true;
+                if (left) open = false;
+                if (got) {
+                    uint32_t rng;
+                    const ray r = camera_sample(J, q, rng);
+                    B.ox[lane] = r.o.x, B.oy[lane] = r.o.y, B.oz[lane] = r.o.z;
+                    B.dx[lane] = r.d.x, B.dy[lane] = r.d.y, B.dz[lane] = r.d.z;
+                    B.tm[lane] = r.t;
+                    B.rng[lane] = rng;
+                    B.q[lane] = q;
                 }
-                given += ok;
-                left -= ok;
+                bl = 0;
+                bh = given;
+                if (!bh) break;
+                __builtin_amdgcn_wave_barrier();
             }
-            if (left) open = false;
-            if (got) {
-                x.r = camera_sample(J, q, x.rng);
+            const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+            const uint32_t avail = bh - bl;
+            if (x.depth == 0 && rank < avail) {
+                const uint32_t k = bl + rank;
+                x.r = ray{d3{B.ox[k], B.oy[k], B.oz[k]}, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
+                x.rng = B.rng[k];
+                x.q = B.q[k];
                 x.thr = d3{1.0, 1.0, 1.0};
                 x.depth = (uint32_t)J.max_depth;
-                x.q = q;
             }
+            bl += min((uint32_t)__popcll(m), avail);
+            __builtin_amdgcn_wave_barrier();
         }
         if (!__any(x.depth != 0)) break;
         pf.mark(PS_LOAD);
