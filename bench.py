@@ -63,7 +63,7 @@ def parse():
 def cpu_baseline(args, threads: int):
     """Time the reference's own code (oracle/_ref/rtw_ref) -- or, when absent,
     the C restatement -- on a bounded sample of the same workload."""
-    spp = args.cpu_spp or 16
+    spp = args.cpu_spp or 32
     ref = ROOT / "oracle" / "_ref" / "rtw_ref"
     sample = f"{args.scene} {args.nx}x{args.ny}x{spp}spp depth {args.depth} (full image, {spp} of the workload's spp)"
     if ref.exists():

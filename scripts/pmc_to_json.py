@@ -1,0 +1,50 @@
+"""Fold the rocprofv3 --pmc passes of scripts/pmc_passes.sh into
+profiles/pmc_intersect.json for the roofline kernel.
+
+HBM bytes per launch follow MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE
+and WRITE_SIZE are KiB from the L2's fabric request counters, FETCH_SIZE
+counted at half the bytes of wide streaming reads (x2 here), each from its own
+pass.  SQ cycle counters are in units of 4 cycles.
+Usage: python scripts/pmc_to_json.py <kernel-substring> <out.json> <segments-per-launch> DIR...
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+kern, out, seg_per_launch, dirs = sys.argv[1], sys.argv[2], float(sys.argv[3]), sys.argv[4:]
+tot = defaultdict(float)
+disp = defaultdict(set)
+for d in dirs:
+    for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+        if kern not in r["Kernel_Name"]:
+            continue
+        tot[r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[r["Counter_Name"]].add((d, r["Dispatch_Id"]))
+per = {k: v / max(1, len(disp[k])) for k, v in tot.items()}  # per launch
+fetch = per.get("FETCH_SIZE", 0.0) * 1024 * 2
+write = per.get("WRITE_SIZE", 0.0) * 1024
+wave_segments = seg_per_launch / 64
+res = {
+    "kernel": kern,
+    "source": "rocprofv3 --kernel-trace --pmc, one pass per counter group (scripts/pmc_passes.sh)",
+    "launches_per_pass": max((len(v) for v in disp.values()), default=0),
+    "hbm_bytes_per_launch": fetch + write,
+    "fetch_bytes_per_launch": fetch,
+    "write_bytes_per_launch": write,
+    "segments_per_launch": seg_per_launch,
+    "valu_insts_per_wave_segment": per.get("SQ_INSTS_VALU", 0) / wave_segments if wave_segments else None,
+    "salu_insts_per_wave_segment": per.get("SQ_INSTS_SALU", 0) / wave_segments if wave_segments else None,
+    "f64_insts_per_wave_segment": {k[14:]: per.get(k, 0) / wave_segments for k in
+                                   ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+                                    "SQ_INSTS_VALU_TRANS_F64")} if wave_segments else None,
+    "wave_cycle_split": {
+        "active_inst_any": per.get("SQ_ACTIVE_INST_ANY", 0) / max(1, per.get("SQ_WAVE_CYCLES", 1)),
+        "wait_inst_any (issue stall)": per.get("SQ_WAIT_INST_ANY", 0) / max(1, per.get("SQ_WAVE_CYCLES", 1)),
+        "wait_any (waitcnt)": per.get("SQ_WAIT_ANY", 0) / max(1, per.get("SQ_WAVE_CYCLES", 1)),
+    },
+    "waves_per_launch": per.get("SQ_WAVES"),
+    "raw_per_launch": per,
+}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps({k: res[k] for k in ("hbm_bytes_per_launch", "valu_insts_per_wave_segment", "wave_cycle_split")}))
