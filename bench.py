@@ -40,6 +40,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # reach HBM: the kernel is fp64-VALU / latency bound.
 
 
+# fp64 VALU issue peak: 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction
+VALU_PEAK_GINST = 1024 * 2.4 / 4
+
+
+def workload_name(args) -> str:
+    name = f"{args.scene} {args.nx}x{args.ny} {args.spp}spp/GPU max_depth {args.depth}" + (" bvh" if args.bvh else "")
+    if (args.scene, args.nx, args.ny, args.spp, args.depth, args.bvh) == ("cornell_box", 800, 800, 1024, 50, False):
+        name += " (north-star target T)"
+    return name
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -171,27 +182,40 @@ def main():
         roofline = None
         if collect and ms_all > 0:
             achieved = algo_all / (ms_all * 1e-3) / 1e9
-            traffic = None
+            traffic, valu = None, None
             pmc = ROOT / "profiles" / "pmc_intersect.json"
+            workload = workload_name(args)
             if pmc.exists():
                 try:
-                    traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
+                    p = json.loads(pmc.read_text())
+                except ValueError:
+                    p = {}
+                # PMC figures only describe the workload (and kernel) they were taken on
+                if p.get("workload") == workload and p.get("kernel") == kernel:
+                    # per launch, scaled from the profiled launches by traversals
+                    scale = (seg_all / max(launches_all, 1)) / p["segments_per_launch"]
+                    traffic = round(p["hbm_bytes_per_launch"] * scale, 1)
+                    ipw = p.get("valu_insts_per_wave_segment")
+                    if ipw:
+                        ach = ipw * seg_all / 64 / (ms_all * 1e-3) / 1e9
+                        valu = {"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST,
+                                "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_GINST, 4),
+                                "insts_per_wave_segment": round(ipw, 1),
+                                "source": "profiles/pmc_intersect.json (SQ_INSTS_VALU)"}
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "kernel": kernel, "launches": int(launches_all),
                         "avg_launch_ms": round(ms_all / max(launches_all, 1), 4),
                         "algo_bytes_per_launch": round(algo_all / max(launches_all, 1), 1),
                         "bytes_per_segment": round(algo_all / max(seg_all, 1), 2)}
+            if valu:
+                roofline["valu"] = valu
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"{args.scene} {nx}x{ny} {spp}spp/GPU max_depth {depth}"
-                                   + (" (north-star target T)" if (args.scene, nx, ny, spp, depth) ==
-                                      ("cornell_box", 800, 800, 1024, 50) else ""),
+            "config": {"workload": workload_name(args),
                        "scene": args.scene, "nx": nx, "ny": ny, "spp_per_gpu": spp, "max_depth": depth,
                        "bvh": args.bvh, "parallelism": f"spp-shard x{world} + RCCL reduce"},
             "msegments_per_s": round(seg_all / args.steps / (elapsed / args.steps) / 1e6, 2) if seg_all else None,

@@ -172,21 +172,30 @@ RTW_D rtw_prim uprim(const rtw_prim* P, int i) {
     return q;
 }
 
-RTW_D rtw_entry uentry(const rtw_entry* E, int i) {
-    rtw_entry e;
-    e.kind = ld(&E[i].kind);
-    e.first_prim = ld(&E[i].first_prim);
-    e.n_prims = ld(&E[i].n_prims);
-    e.n_ops = ld(&E[i].n_ops);
-#pragma unroll
-    for (int k = 0; k < RTW_MAX_OPS; ++k) {
-        e.op[k] = ld(&E[i].op[k]);
-#pragma unroll
-        for (int a = 0; a < 3; ++a) e.op_param[k][a] = ld(&E[i].op_param[k][a]);
-    }
-    e.phase_material = ld(&E[i].phase_material);
-    e.bvh_root = ld(&E[i].bvh_root);
-    e.density = ld(&E[i].density);
+// Loads that are scalar (s_load through the constant address space) when
+// U, i.e. when the index is wave-uniform, else ordinary per-lane loads.
+template <bool U, typename T>
+RTW_D T rd(const T* p) {
+    if constexpr (U) return ld(p);
+    else return *p;
+}
+
+// A world-list entry as the kernels use it: the header in registers; op
+// types and parameters (up to 4 ops x 3 doubles) read where an op is applied,
+// not all up front.
+struct entry_v {
+    const rtw_entry* p;
+    int kind, first_prim, n_prims, n_ops, bvh_root;
+};
+template <bool U>
+RTW_D entry_v view_entry(const rtw_entry* E, int i) {
+    entry_v e;
+    e.p = E + i;
+    e.kind = rd<U>(&E[i].kind);
+    e.first_prim = rd<U>(&E[i].first_prim);
+    e.n_prims = rd<U>(&E[i].n_prims);
+    e.n_ops = rd<U>(&E[i].n_ops);
+    e.bvh_root = rd<U>(&E[i].bvh_root);
     return e;
 }
 
@@ -255,11 +264,13 @@ RTW_D d3 rect_normal(int type) {
 }
 
 // translate::hit hittable.h:299-311, rotate_y::hit :373-404 (ray inward)
-RTW_D void op_ray_in(int op, const double* q, ray& r) {
+template <bool U>
+RTW_D void op_ray_in(const rtw_entry* E, int k, ray& r) {
+    const int op = rd<U>(&E->op[k]);
     if (op == RTW_OP_TRANSLATE) {
-        r.o = r.o - ld3(q);
+        r.o = r.o - d3{rd<U>(&E->op_param[k][0]), rd<U>(&E->op_param[k][1]), rd<U>(&E->op_param[k][2])};
     } else if (op == RTW_OP_ROTATE_Y) {
-        const double s = q[0], c = q[1];
+        const double s = rd<U>(&E->op_param[k][0]), c = rd<U>(&E->op_param[k][1]);
         const d3 o = r.o, d = r.d;
         r.o.x = c * o.x - s * o.z;
         r.o.z = s * o.x + c * o.z;
@@ -268,11 +279,13 @@ RTW_D void op_ray_in(int op, const double* q, ray& r) {
     }
 }
 // ... and the record outward (p, normal), innermost op first
-RTW_D void op_rec_out(int op, const double* q, d3& p, d3& n) {
+template <bool U>
+RTW_D void op_rec_out(const rtw_entry* E, int k, d3& p, d3& n) {
+    const int op = rd<U>(&E->op[k]);
     if (op == RTW_OP_TRANSLATE) {
-        p = p + ld3(q);
+        p = p + d3{rd<U>(&E->op_param[k][0]), rd<U>(&E->op_param[k][1]), rd<U>(&E->op_param[k][2])};
     } else if (op == RTW_OP_ROTATE_Y) {
-        const double s = q[0], c = q[1];
+        const double s = rd<U>(&E->op_param[k][0]), c = rd<U>(&E->op_param[k][1]);
         const d3 p0 = p, n0 = n;
         p.x = c * p0.x + s * p0.z;
         p.z = -s * p0.x + c * p0.z;
@@ -284,16 +297,18 @@ RTW_D void op_rec_out(int op, const double* q, d3& p, d3& n) {
 }
 
 // Statically indexed op chain (no runtime-indexed register arrays).
-RTW_D ray entry_local_ray(const rtw_entry& e, ray r) {
+template <bool U>
+RTW_D ray entry_local_ray(const entry_v& e, ray r) {
 #pragma unroll
     for (int k = 0; k < RTW_MAX_OPS; ++k)
-        if (k < e.n_ops) op_ray_in(e.op[k], e.op_param[k], r);
+        if (k < e.n_ops) op_ray_in<U>(e.p, k, r);
     return r;
 }
-RTW_D void entry_rec_out(const rtw_entry& e, d3& p, d3& n) {
+template <bool U>
+RTW_D void entry_rec_out(const entry_v& e, d3& p, d3& n) {
 #pragma unroll
     for (int k = RTW_MAX_OPS - 1; k >= 0; --k)
-        if (k < e.n_ops) op_rec_out(e.op[k], e.op_param[k], p, n);
+        if (k < e.n_ops) op_rec_out<U>(e.p, k, p, n);
 }
 
 // ------------------------------------------------------------------ traversal
@@ -397,7 +412,7 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
 }
 
 template <int F>
-RTW_D void group_closest(const scene& S, const rtw_entry& e, const ray& r, double t_min, hit_state& h) {
+RTW_D void group_closest(const scene& S, const entry_v& e, const ray& r, double t_min, hit_state& h) {
     if ((F & F_GBVH) && e.bvh_root >= 0)
         group_bvh(S, e.bvh_root, r, t_min, h);
     else
@@ -407,8 +422,8 @@ RTW_D void group_closest(const scene& S, const rtw_entry& e, const ray& r, doubl
 // Closest t of a medium's boundary in (t0, t1) (hittable.h:438-449); the
 // boundary is the entry's ops + group.
 template <int F>
-RTW_D bool boundary_t(const scene& S, const rtw_entry& e, const ray& r, double t0, double t1, double& t) {
-    const ray lr = entry_local_ray(e, r);
+RTW_D bool boundary_t(const scene& S, const entry_v& e, const ray& r, double t0, double t1, double& t) {
+    const ray lr = entry_local_ray<true>(e, r);
     hit_state h{t1, -1, false};
     group_closest<F>(S, e, lr, t0, h);
     if (h.prim == -1) return false;
@@ -418,7 +433,7 @@ RTW_D bool boundary_t(const scene& S, const rtw_entry& e, const ray& r, double t
 
 // constant_medium::hit hittable.h:430-479 (at most one draw per call)
 template <int F>
-RTW_D bool medium_t(const scene& S, const rtw_entry& e, const ray& r, double t_min, double t_max, uint32_t& rng,
+RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& r, double t_min, double t_max, uint32_t& rng,
                     double& t_out) {
     double t1, t2;
     if (!boundary_t<F>(S, e, r, -kDblMax, kDblMax, t1)) return false;
@@ -429,7 +444,7 @@ RTW_D bool medium_t(const scene& S, const rtw_entry& e, const ray& r, double t_m
     if (t1 < 0) t1 = 0;
     const double dl = len(r.d);
     const double inside = (t2 - t1) * dl;
-    const double hit_distance = -(1 / e.density) * log(rnd01(rng));
+    const double hit_distance = -(1 / rd<true>(&e.p->density)) * log(rnd01(rng));
     if (hit_distance < inside) {
         t_out = t1 + hit_distance / dl;
         return true;
@@ -455,8 +470,8 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
             if (!slab(nd, r.o, inv, widen_lo(kTMin), widen_hi(h.t))) continue;
             if (nd.count > 0) {
                 for (int k = 0; k < nd.count; ++k) {
-                    const rtw_entry e = S.entries[S.items[nd.left + k]];
-                    const ray lr = entry_local_ray(e, r);
+                    const entry_v e = view_entry<false>(S.entries, S.items[nd.left + k]);
+                    const ray lr = entry_local_ray<false>(e, r);
                     if ((F & F_GBVH) && e.bvh_root >= 0) {
                         group_bvh(S, e.bvh_root, lr, kTMin, h);
                     } else {
@@ -471,7 +486,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
         return h;
     } else {
         for (int ei = 0; ei < S.n_entries; ++ei) {
-            const rtw_entry e = uentry(S.entries, ei);
+            const entry_v e = view_entry<true>(S.entries, ei);
             if ((F & F_MEDIA) && e.kind == RTW_ENTRY_MEDIUM) {
                 double t;
                 if (medium_t<F>(S, e, r, kTMin, h.t, rng, t)) {
@@ -481,13 +496,13 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
                 }
                 continue;
             }
-            const ray lr = entry_local_ray(e, r);
+            const ray lr = entry_local_ray<true>(e, r);
             group_closest<F>(S, e, lr, kTMin, h);
         }
         if (F & F_MEDIA) {
             for (int k = 0; k < S.n_media; ++k) {
                 const int ei = ld(&S.media[k]);
-                const rtw_entry e = uentry(S.entries, ei);
+                const entry_v e = view_entry<true>(S.entries, ei);
                 double t;
                 if (medium_t<F>(S, e, r, kTMin, h.t, rng, t)) {
                     h.t = t;
@@ -504,15 +519,14 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
 // the reference produced it (leaf hit, then ops outward).
 RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d3& n, int& mat) {
     if (h.prim <= -2) {  // constant_medium, hittable.h:469-472
-        const rtw_entry& e = S.entries[-h.prim - 2];
         p = at(r, h.t);
         n = d3{1, 0, 0};
-        mat = e.phase_material;
+        mat = S.entries[-h.prim - 2].phase_material;
         return;
     }
     const rtw_prim q = S.prims[h.prim];
-    const rtw_entry e = S.entries[q.entry];
-    const ray lr = entry_local_ray(e, r);
+    const entry_v e = view_entry<false>(S.entries, q.entry);
+    const ray lr = entry_local_ray<false>(e, r);
     p = at(lr, h.t);
     if (is_sphere(q.type)) {
         const d3 cc = sphere_center(q, lr.t);
@@ -521,7 +535,7 @@ RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d
         n = rect_normal(q.type);
     }
     if (q.flip & 1) n = -n;
-    entry_rec_out(e, p, n);
+    entry_rec_out<false>(e, p, n);
     mat = q.material;
 }
 

@@ -91,7 +91,7 @@ __host__ __device__ inline uint64_t shard_limit(int s, uint64_t total) {
 }
 
 struct job_t {
-    rtw_camera_desc cam;
+    const rtw_camera_desc* cam;  // device copy (read where rays are made, see camera_sample)
     uint64_t seed_mix;   // splitmix64(seed)
     uint32_t total;      // samples in this pass
     uint32_t npix;       // pixels of this call (n_rows * nx)
@@ -117,7 +117,25 @@ __device__ __forceinline__ ray camera_sample(const job_t& J, uint32_t q, uint32_
     rng = path_seed(J.seed_mix, (uint32_t)(j * J.nx + i), (uint32_t)s);
     const double u = (double)(i + rnd01(rng)) / (double)J.nx;
     const double v = (double)(j + rnd01(rng)) / (double)J.ny;
-    return camera_ray(J.cam, u, v, rng);
+    // The camera (23 doubles) is loaded here, with scalar loads, each time
+    // rays are made: an opaque pointer stops the compiler from hoisting it
+    // into loop-carried SGPRs of the persistent loop, where it spills.
+    const rtw_camera_desc* cp = J.cam;
+    asm volatile("" : "+s"(cp));
+    rtw_camera_desc c;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        c.origin[k] = ld(&cp->origin[k]);
+        c.lower_left[k] = ld(&cp->lower_left[k]);
+        c.horizontal[k] = ld(&cp->horizontal[k]);
+        c.vertical[k] = ld(&cp->vertical[k]);
+        c.u[k] = ld(&cp->u[k]);
+        c.v[k] = ld(&cp->v[k]);
+    }
+    c.time0 = ld(&cp->time0);
+    c.time1 = ld(&cp->time1);
+    c.lens_radius = ld(&cp->lens_radius);
+    return camera_ray(c, u, v, rng);
 }
 
 __device__ __forceinline__ void raygen(const job_t& J, const fresh_t& F, uint32_t k, uint32_t q) {
@@ -518,9 +536,11 @@ struct ray_batch {  // one wave's buffer of generated camera samples (LDS)
     uint32_t rng[64], q[64];
 };
 
+// The all-features instantiations would take ~210-230 VGPRs (2 waves per
+// SIMD); capping them at 3 waves costs a handful of spilled registers.
 template <int F, int M, bool LDS>
-__global__ __launch_bounds__(kBlock) RTW_SEG_ATTR void k_persist(scene S, job_t J, ctrs_t* C, const char* base,
-                                                                 uint32_t bytes) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M == SF_ALL ? 3 : 1)))
+void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kWaves];
     __shared__ ray_batch s_batch[kWaves];
@@ -844,6 +864,8 @@ struct handle_t {
     dev_buf run;      // per-pixel running sums
     dev_buf accum;    // device accum when the caller passes a host pointer
     dev_buf ctrs;
+    dev_buf camera;                // device copy of the call's camera
+    rtw_camera_desc cam_host{};    // its source (lives until the copy ran)
     ctrs_t* host_ctrs = nullptr;  // pinned
     uint32_t pool_cap = 0;
     int grid = 2048;
@@ -1021,12 +1043,29 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
                                st, S, J, C, base, bytes);                                                   \
         return true;                                                                                       \
     }
+    // specialised: small list scenes whose shading data fit in LDS, and the
+    // lambertian / metal / dielectric sets of the Book-1 scene, flat or BVH
     RTW_PER(0, SF_DIEL, true)
     RTW_PER(0, SF_METAL | SF_DIEL, true)
     RTW_PER(0, SF_ALL, true)
-    RTW_PER(0, SF_ALL, false)
-    RTW_PER(F_WBVH, SF_ALL, false)
-    RTW_PER(F_WBVH, SF_ALL, true)
+    RTW_PER(0, SF_METAL | SF_DIEL, false)
+    RTW_PER(F_WBVH, SF_METAL | SF_DIEL, false)
+#undef RTW_PER
+    // general: every material / texture, scene read through the caches, one
+    // instantiation per traversal feature set (a world BVH never holds media)
+#define RTW_PER(FF)                                                                                           \
+    if (f == (FF)) {                                                                                        \
+        if (!probe)                                                                                         \
+            hipLaunchKernelGGL((k_persist<FF, SF_ALL, false>), dim3(persist_grid<FF, SF_ALL, false>(0, cus)),  \
+                               dim3(kBlock), 0, st, S, J, C, base, bytes);                                  \
+        return true;                                                                                       \
+    }
+    RTW_PER(0)
+    RTW_PER(F_MEDIA)
+    RTW_PER(F_WBVH)
+    RTW_PER(F_GBVH)
+    RTW_PER(F_MEDIA | F_GBVH)
+    RTW_PER(F_WBVH | F_GBVH)
 #undef RTW_PER
     return false;
 }
@@ -1197,6 +1236,7 @@ extern "C" void rtw_scene_free(void* handle) {
     h->run.release();
     h->accum.release();
     h->ctrs.release();
+    h->camera.release();
     if (h->host_ctrs) hipHostFree(h->host_ctrs);
     for (hipEvent_t e : h->events) hipEventDestroy(e);
     if (h->stream) hipStreamDestroy(h->stream);
@@ -1271,7 +1311,10 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     HIPCHK(hipMemsetAsync(C, 0, sizeof(ctrs_t), st));
 
     job_t J;
-    J.cam = *camera;
+    h->cam_host = *camera;
+    if ((rc = h->camera.ensure(sizeof(rtw_camera_desc)))) return rc;
+    HIPCHK(hipMemcpyAsync(h->camera.p, &h->cam_host, sizeof(rtw_camera_desc), hipMemcpyHostToDevice, st));
+    J.cam = static_cast<const rtw_camera_desc*>(h->camera.p);
     J.seed_mix = host_splitmix64(R.seed);
     J.npix = (uint32_t)npix;
     J.nx = R.nx, J.ny = R.ny, J.row_begin = R.row_begin, J.row_step = row_step;

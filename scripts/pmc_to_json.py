@@ -5,14 +5,14 @@ HBM bytes per launch follow MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE
 and WRITE_SIZE are KiB from the L2's fabric request counters, FETCH_SIZE
 counted at half the bytes of wide streaming reads (x2 here), each from its own
 pass.  SQ cycle counters are in units of 4 cycles.
-Usage: python scripts/pmc_to_json.py <kernel-substring> <out.json> <segments-per-launch> DIR...
+Usage: python scripts/pmc_to_json.py <kernel-substring> <out.json> <segments-per-launch> <workload> DIR...
 """
 import csv
 import json
 import sys
 from collections import defaultdict
 
-kern, out, seg_per_launch, dirs = sys.argv[1], sys.argv[2], float(sys.argv[3]), sys.argv[4:]
+kern, out, seg_per_launch, workload, dirs = sys.argv[1], sys.argv[2], float(sys.argv[3]), sys.argv[4], sys.argv[5:]
 tot = defaultdict(float)
 disp = defaultdict(set)
 for d in dirs:
@@ -27,6 +27,7 @@ write = per.get("WRITE_SIZE", 0.0) * 1024
 wave_segments = seg_per_launch / 64
 res = {
     "kernel": kern,
+    "workload": workload,
     "source": "rocprofv3 --kernel-trace --pmc, one pass per counter group (scripts/pmc_passes.sh)",
     "launches_per_pass": max((len(v) for v in disp.values()), default=0),
     "hbm_bytes_per_launch": fetch + write,
