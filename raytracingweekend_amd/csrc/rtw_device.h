@@ -15,6 +15,9 @@
 #include "rtw_div.h"
 
 #define RTW_D __device__ __forceinline__
+// vector helpers also used by the host to precompute per-primitive frames
+// with the very same arithmetic (see upload_scene)
+#define RTW_HD __host__ __device__ __forceinline__
 
 namespace rtwd {
 
@@ -34,21 +37,21 @@ constexpr double kCanonRcp = 1.0 / kCanonDiv;  // RN(1/x): constant folding is I
 struct d3 {
     double x, y, z;
 };
-RTW_D d3 mk(double x, double y, double z) { return d3{x, y, z}; }
-RTW_D d3 operator+(d3 a, d3 b) { return d3{a.x + b.x, a.y + b.y, a.z + b.z}; }
-RTW_D d3 operator-(d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; }
-RTW_D d3 operator*(d3 a, d3 b) { return d3{a.x * b.x, a.y * b.y, a.z * b.z}; }
-RTW_D d3 operator*(d3 a, double s) { return d3{a.x * s, a.y * s, a.z * s}; }
-RTW_D d3 operator/(d3 a, double s) { return d3{a.x / s, a.y / s, a.z / s}; }
-RTW_D d3 operator-(d3 a) { return d3{-a.x, -a.y, -a.z}; }
-RTW_D double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-RTW_D double len2(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-RTW_D double len(d3 a) { return __builtin_sqrt(len2(a)); }
-RTW_D d3 cross(d3 a, d3 b) {  // vec3.h:54-59
+RTW_HD d3 mk(double x, double y, double z) { return d3{x, y, z}; }
+RTW_HD d3 operator+(d3 a, d3 b) { return d3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+RTW_HD d3 operator-(d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+RTW_HD d3 operator*(d3 a, d3 b) { return d3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+RTW_HD d3 operator*(d3 a, double s) { return d3{a.x * s, a.y * s, a.z * s}; }
+RTW_HD d3 operator/(d3 a, double s) { return d3{a.x / s, a.y / s, a.z / s}; }
+RTW_HD d3 operator-(d3 a) { return d3{-a.x, -a.y, -a.z}; }
+RTW_HD double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RTW_HD double len2(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+RTW_HD double len(d3 a) { return __builtin_sqrt(len2(a)); }
+RTW_HD d3 cross(d3 a, d3 b) {  // vec3.h:54-59
     return d3{a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x};
 }
-RTW_D d3 normalize(d3 v) { return v / len(v); }  // vec3.h:61-67
-RTW_D d3 ld3(const double* p) { return d3{p[0], p[1], p[2]}; }
+RTW_HD d3 normalize(d3 v) { return v / len(v); }  // vec3.h:61-67
+RTW_HD d3 ld3(const double* p) { return d3{p[0], p[1], p[2]}; }
 
 struct ray {
     d3 o, d;
@@ -122,7 +125,7 @@ RTW_D d3 random_cosine_direction(uint32_t& s) {  // utility.h:54-67
 struct onb {
     d3 u, v, w;
 };
-RTW_D onb onb_from_w(d3 n) {  // onb.h:32-38
+RTW_HD onb onb_from_w(d3 n) {  // onb.h:32-38
     onb b;
     b.w = normalize(n);
     const d3 a = (fabs(b.w.x) > 0.9) ? d3{0, 1, 0} : d3{1, 0, 0};
@@ -130,7 +133,7 @@ RTW_D onb onb_from_w(d3 n) {  // onb.h:32-38
     b.u = cross(b.w, b.v);
     return b;
 }
-RTW_D d3 local(const onb& b, d3 a) { return b.u * a.x + b.v * a.y + b.w * a.z; }  // onb.h:21-24
+RTW_HD d3 local(const onb& b, d3 a) { return b.u * a.x + b.v * a.y + b.w * a.z; }  // onb.h:21-24
 
 // ------------------------------------------------------------------ scene
 struct scene {
@@ -143,6 +146,7 @@ struct scene {
     const int32_t* items;
     const double* ranvec;
     const int32_t* perm;
+    const double* prim_onb;  // per rect prim: onb of its world normal (u, v, w), host-built
     int32_t n_entries, n_lights, world_bvh_root, render_type, background;
     int32_t has_media;
     int32_t n_media;
@@ -259,7 +263,7 @@ RTW_D bool prim_t(const rtw_prim& q, const ray& r, double t0, double t1, double&
     return is_sphere(q.type) ? sphere_t(q, r, t0, t1, t_out) : rect_t(q, r, t0, t1, t_out);
 }
 
-RTW_D d3 rect_normal(int type) {
+RTW_HD d3 rect_normal(int type) {
     return type == RTW_PRIM_RECT_XY ? d3{0, 0, 1} : (type == RTW_PRIM_RECT_XZ ? d3{0, 1, 0} : d3{1, 0, 0});
 }
 
@@ -517,7 +521,8 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
 
 // Reconstruct the hit record (p, normal, material) of a winner exactly as
 // the reference produced it (leaf hit, then ops outward).
-RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d3& n, int& mat) {
+RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d3& n, int& mat, bool& rect) {
+    rect = false;
     if (h.prim <= -2) {  // constant_medium, hittable.h:469-472
         p = at(r, h.t);
         n = d3{1, 0, 0};
@@ -533,6 +538,7 @@ RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d
         n = (p - cc) / q.p[3];
     } else {
         n = rect_normal(q.type);
+        rect = true;
     }
     if (q.flip & 1) n = -n;
     entry_rec_out<false>(e, p, n);

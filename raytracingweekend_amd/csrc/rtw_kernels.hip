@@ -320,7 +320,8 @@ __device__ __forceinline__ bool shade_core(const scene& S, path_st& x, double t,
     }
     d3 p, n;
     int mat;
-    hit_record(S, r, hit_state{t, prim, false}, p, n, mat);
+    bool rect;
+    hit_record(S, r, hit_state{t, prim, false}, p, n, mat, rect);
     if (S.render_type == RTW_RENDER_NORMAL) {  // :135-136
         L = thr * (d3{0.5f, 0.5f, 0.5f} * (n + d3{1, 1, 1}));
         return true;
@@ -360,7 +361,15 @@ __device__ __forceinline__ bool shade_core(const scene& S, path_st& x, double t,
         f = texture_value<M>(S, m.texture, p);
     } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
         const d3 att = texture_value<M>(S, m.texture, p);
-        const onb uvw = onb_from_w(n);
+        // onb::build_from_w(normal) (onb.h:32-38): a rect's world normal is
+        // fixed, so its frame comes from the host-built table (same arithmetic)
+        onb uvw;
+        if (rect) {
+            const double* f = S.prim_onb + 9 * (size_t)prim;
+            uvw.u = ld3(f), uvw.v = ld3(f + 3), uvw.w = ld3(f + 6);
+        } else {
+            uvw = onb_from_w(n);
+        }
         pf.mark(PS_HIT);
         double pdf_val;
         if (S.n_lights > 0) {  // mixture_pdf(cosine_pdf, hittable_pdf(lights)) pdf.h:55-79
@@ -430,6 +439,7 @@ __device__ __forceinline__ scene lds_scene(const scene& S, const char* base, con
     L.ranvec = (const double*)rb(S.ranvec);
     L.perm = (const int32_t*)rb(S.perm);
     L.media = (const int32_t*)rb(S.media);
+    L.prim_onb = (const double*)rb(S.prim_onb);
     return L;
 }
 
@@ -914,8 +924,35 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         size_t bytes;
         size_t off;
     };
+    // World-space onb of every rect primitive's normal: rect_normal, the
+    // prim's own flip, then its entry's ops outward -- hit_record's normal
+    // path (rtw_device.h) -- and onb_from_w, all with the device's expressions.
+    std::vector<double> frames((size_t)d->n_prims * 9, 0.0);
+    for (int pi = 0; pi < d->n_prims; ++pi) {
+        const rtw_prim& q = d->prims[pi];
+        if (q.type < RTW_PRIM_RECT_XY || q.entry < 0) continue;
+        d3 n = rect_normal(q.type);
+        if (q.flip & 1) n = -n;
+        const rtw_entry& e = d->entries[q.entry];
+        for (int k = RTW_MAX_OPS - 1; k >= 0; --k) {
+            if (k >= e.n_ops) continue;
+            if (e.op[k] == RTW_OP_ROTATE_Y) {
+                const double s = e.op_param[k][0], c = e.op_param[k][1];
+                const d3 n0 = n;
+                n.x = c * n0.x + s * n0.z;
+                n.z = -s * n0.x + c * n0.z;
+            } else if (e.op[k] == RTW_OP_FLIP) {
+                n = -n;
+            }
+        }
+        const onb b = onb_from_w(n);
+        double* f = frames.data() + 9 * (size_t)pi;
+        f[0] = b.u.x, f[1] = b.u.y, f[2] = b.u.z;
+        f[3] = b.v.x, f[4] = b.v.y, f[5] = b.v.z;
+        f[6] = b.w.x, f[7] = b.w.y, f[8] = b.w.z;
+    }
     std::vector<part> parts = {
-        // parts 0..7 are what shading reads; they come first so a small
+        // parts 0..8 are what shading reads; they come first so a small
         // scene's shading data is one contiguous prefix the shade kernel can
         // stage in LDS
         {d->prims, sizeof(rtw_prim) * d->n_prims, 0},
@@ -926,6 +963,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {d->has_perlin ? d->perlin_ranvec : nullptr, d->has_perlin ? sizeof(double) * 768 : 0, 0},
         {d->has_perlin ? d->perlin_perm : nullptr, d->has_perlin ? sizeof(int32_t) * 768 : 0, 0},
         {media.data(), sizeof(int32_t) * media.size(), 0},
+        {frames.data(), sizeof(double) * frames.size(), 0},
         {d->bvh_nodes, sizeof(rtw_bvh_node) * d->n_bvh_nodes, 0},
         {d->bvh_items, sizeof(int32_t) * d->n_bvh_items, 0},
     };
@@ -951,9 +989,10 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.ranvec = (const double*)at(5);
     S.perm = (const int32_t*)at(6);
     S.media = (const int32_t*)at(7);
-    S.nodes = (const rtw_bvh_node*)at(8);
-    S.items = (const int32_t*)at(9);
-    h->shade_bytes = (uint32_t)parts[8].off;  // the shading prefix
+    S.prim_onb = (const double*)at(8);
+    S.nodes = (const rtw_bvh_node*)at(9);
+    S.items = (const int32_t*)at(10);
+    h->shade_bytes = (uint32_t)parts[9].off;  // the shading prefix
     h->scene_base = base;
     S.n_entries = d->n_entries;
     S.n_lights = d->n_lights;
