@@ -546,10 +546,16 @@ struct ray_batch {  // one wave's buffer of generated camera samples (LDS)
     uint32_t rng[64], q[64];
 };
 
-// The all-features instantiations would take ~210-230 VGPRs (2 waves per
-// SIMD); capping them at 3 waves costs a handful of spilled registers.
+// Occupancy: left alone the compiler gives k_persist 160-230 VGPRs (2-3
+// waves per SIMD).  Capping at 128 (4 waves) costs some spilled registers and
+// wins: 2 638 -> 2 980 Msamples/s on Cornell (5 waves spill too much: 2 578).
+#ifdef RTW_SEG_WAVES
+#define RTW_PERSIST_WAVES(M) RTW_SEG_WAVES
+#else
+#define RTW_PERSIST_WAVES(M) 4
+#endif
 template <int F, int M, bool LDS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M == SF_ALL ? 3 : 1)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(M))))
 void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kWaves];
