@@ -294,45 +294,49 @@ __device__ __forceinline__ d3 background(const scene& S, const d3& dir) {
     return d3{1.0, 1.0, 1.0} * (1.0 - t) + d3{0.5f, 0.7f, 1.0} * t;  // lerp, vec3.h:84-87
 }
 
-// A path between two color() calls: the ray of the next call, the product
-// of the attenuation / pdf factors so far, its engine, the depth argument of
-// the next call and its sample id.
+// A path between two color() calls: the ray of the next call, its engine,
+// the depth argument of the next call and its sample id.  (The throughput,
+// the product of the attenuation / pdf factors so far, is kept by the caller:
+// the persistent kernel parks it in LDS, out of the register budget.)
 struct path_st {
     ray r;
-    d3 thr;
     uint32_t rng, depth, q;
 };
 
+// Outcome of one segment: the path continues with throughput *= f, or ends
+// with radiance thr * E, or ends with radiance 0.
+enum { SEG_CONTINUE = 0, SEG_END = 1, SEG_END_ZERO = 2 };
+
 // One segment of color() (RayTracingWeekend.cpp:52-159) for path x whose
-// world hit is (t, prim).  Returns true when the path ends (its radiance in
-// L); otherwise x becomes the scattered path.  The recursion's inside-out
-// products are folded forward: L = thr * (last emitted / background), with
-// the reference's per-bounce factor attenuation * scattering_pdf / pdf.
+// world hit is (t, prim).  The recursion's inside-out products are folded
+// forward: the radiance of a path is thr * (last emitted / background), thr
+// the product of the reference's per-bounce factors attenuation *
+// scattering_pdf / pdf (or attenuation for specular scatter).
 template <int M>
-__device__ __forceinline__ bool shade_core(const scene& S, path_st& x, double t, int32_t prim, d3& L, prof_t& pf) {
+__device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, int32_t prim, d3& E, d3& f,
+                                          prof_t& pf) {
     const ray r = x.r;
-    const d3 thr = x.thr;
     uint32_t rng = x.rng;
     const uint32_t depth = x.depth;
     if (prim == -1) {
-        L = thr * background(S, r.d);
-        return true;
+        E = background(S, r.d);
+        return SEG_END;
     }
     d3 p, n;
     int mat;
     bool rect;
     hit_record(S, r, hit_state{t, prim, false}, p, n, mat, rect);
     if (S.render_type == RTW_RENDER_NORMAL) {  // :135-136
-        L = thr * (d3{0.5f, 0.5f, 0.5f} * (n + d3{1, 1, 1}));
-        return true;
+        E = d3{0.5f, 0.5f, 0.5f} * (n + d3{1, 1, 1});
+        return SEG_END;
     }
     const rtw_material& m = S.materials[mat];
     pf.mark(PS_HIT);
     d3 dir;
-    d3 f;  // throughput factor of this bounce
     if (m.type == RTW_MAT_DIFFUSE_LIGHT) {  // material.h:232-244: no scatter
-        L = (dot(n, r.d) > 0) ? thr * texture_value<M>(S, m.texture, p) : d3{0, 0, 0};
-        return true;
+        if (!(dot(n, r.d) > 0)) return SEG_END_ZERO;
+        E = texture_value<M>(S, m.texture, p);
+        return SEG_END;
     } else if ((M & SF_METAL) && m.type == RTW_MAT_METAL) {  // material.h:128-136
         const d3 reflected = reflect(normalize(r.d), n);
         dir = reflected + random_in_unit_sphere(rng) * m.fuzz;
@@ -360,7 +364,6 @@ __device__ __forceinline__ bool shade_core(const scene& S, path_st& x, double t,
         dir = random_in_unit_sphere(rng);
         f = texture_value<M>(S, m.texture, p);
     } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
-        const d3 att = texture_value<M>(S, m.texture, p);
         // onb::build_from_w(normal) (onb.h:32-38): a rect's world normal is
         // fixed, so its frame comes from the host-built table (same arithmetic)
         onb uvw;
@@ -383,24 +386,19 @@ __device__ __forceinline__ bool shade_core(const scene& S, path_st& x, double t,
             const double cw = dot(normalize(dir), uvw.w);
             pdf_val = (cw <= 0) ? 0 : cw / kPi;
         }
-        if (pdf_val <= 0.0) {  // :126-127 returns emitted (= 0)
-            L = d3{0, 0, 0};
-            return true;
-        }
+        if (pdf_val <= 0.0) return SEG_END_ZERO;  // :126-127 returns emitted (= 0)
         const double cosine = dot(n, normalize(dir));  // material.h:115-119
         const double spdf = cosine < 0 ? 0 : cosine / kPi;
-        f = (att * spdf) / pdf_val;
+        // attenuation = texture value (material.h:98), read only now: it
+        // draws nothing, and a late read keeps it out of the busiest registers
+        f = (texture_value<M>(S, m.texture, p) * spdf) / pdf_val;
         pf.mark(PS_PDF);
     }
-    if (depth <= 1) {  // the next color() call has depth 0 and returns 0
-        L = d3{0, 0, 0};
-        return true;
-    }
+    if (depth <= 1) return SEG_END_ZERO;  // the next color() call has depth 0 and returns 0
     x.r = ray{p, dir, r.t};
-    x.thr = thr * f;
     x.rng = rng;
     x.depth = depth - 1;
-    return false;
+    return SEG_CONTINUE;
 }
 
 // The wavefront form: path x (read from pool slot i or, fresh, from staging)
@@ -411,16 +409,26 @@ __device__ __forceinline__ bool shade_one(const scene& S, const job_t& J, const 
                                           uint32_t& q, prof_t& pf) {
     path_st s;
     s.r = x.r;
-    s.thr = x.fresh ? d3{1.0, 1.0, 1.0} : d3{P.tr[i], P.tg[i], P.tb[i]};
     s.rng = rng;
     s.depth = x.fresh ? (uint32_t)J.max_depth : x.depth;
     s.q = x.fresh ? FR.qid[x.src] : P.qid[i];
     q = s.q;
-    if (shade_core<M>(S, s, t, prim, L, pf)) return true;
+    d3 E, f;
+    const int out = shade_core<M>(S, s, t, prim, E, f, pf);
+    const d3 thr = x.fresh ? d3{1.0, 1.0, 1.0} : d3{P.tr[i], P.tg[i], P.tb[i]};
+    if (out == SEG_END) {
+        L = thr * E;
+        return true;
+    }
+    if (out == SEG_END_ZERO) {
+        L = d3{0, 0, 0};
+        return true;
+    }
+    const d3 nt = thr * f;
     P.ox[i] = s.r.o.x, P.oy[i] = s.r.o.y, P.oz[i] = s.r.o.z;
     P.dx[i] = s.r.d.x, P.dy[i] = s.r.d.y, P.dz[i] = s.r.d.z;
     P.tm[i] = s.r.t;
-    P.tr[i] = s.thr.x, P.tg[i] = s.thr.y, P.tb[i] = s.thr.z;
+    P.tr[i] = nt.x, P.tg[i] = nt.y, P.tb[i] = nt.z;
     P.rng[i] = s.rng;
     P.depth[i] = s.depth;
     P.qid[i] = s.q;
@@ -560,6 +568,7 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kWaves];
     __shared__ ray_batch s_batch[kWaves];
+    __shared__ double s_thr[3][kBlock];  // each lane's path throughput
     if (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(base);
         uint4* dst = reinterpret_cast<uint4*>(s_scene);
@@ -626,7 +635,7 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
                 x.r = ray{d3{B.ox[k], B.oy[k], B.oz[k]}, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
                 x.rng = B.rng[k];
                 x.q = B.q[k];
-                x.thr = d3{1.0, 1.0, 1.0};
+                s_thr[0][threadIdx.x] = 1.0, s_thr[1][threadIdx.x] = 1.0, s_thr[2][threadIdx.x] = 1.0;
                 x.depth = (uint32_t)J.max_depth;
             }
             bl += min((uint32_t)__popcll(m), avail);
@@ -638,8 +647,14 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
             const hit_state h = world_closest<F>(S, x.r, x.rng);
             pf.mark(PS_TRAVERSE);
             ++segs;
-            d3 L;
-            if (shade_core<M>(SS, x, h.t, h.prim, L, pf)) {
+            d3 E, f;
+            const int out = shade_core<M>(SS, x, h.t, h.prim, E, f, pf);
+            const d3 thr{s_thr[0][threadIdx.x], s_thr[1][threadIdx.x], s_thr[2][threadIdx.x]};
+            if (out == SEG_CONTINUE) {
+                const d3 nt = thr * f;
+                s_thr[0][threadIdx.x] = nt.x, s_thr[1][threadIdx.x] = nt.y, s_thr[2][threadIdx.x] = nt.z;
+            } else {
+                const d3 L = out == SEG_END ? thr * E : d3{0, 0, 0};
                 double* o = J.L + 3 * (size_t)x.q;
                 o[0] = L.x, o[1] = L.y, o[2] = L.z;
                 x.depth = 0;
