@@ -13,6 +13,7 @@
 #include <stdint.h>
 #include "rtw_gpu.h"
 #include "rtw_div.h"
+#include "rtw_math.h"
 
 #define RTW_D __device__ __forceinline__
 // vector helpers also used by the host to precompute per-primitive frames
@@ -117,7 +118,7 @@ RTW_D d3 random_cosine_direction(uint32_t& s) {  // utility.h:54-67
     const double phi = kTwoPi * r1;
     const double sq = __builtin_sqrt(r2);
     double sp, cp;
-    sincos(phi, &sp, &cp);
+    sincos_azimuth(phi, sp, cp);
     return d3{cp * sq, sp * sq, z};
 }
 
@@ -147,6 +148,8 @@ struct scene {
     const double* ranvec;
     const int32_t* perm;
     const double* prim_onb;  // per rect prim: onb of its world normal (u, v, w), host-built
+    const double* mat_aux;   // per material: 1/ref_idx, schlick's r0^2 (host-built, same expressions)
+    double light_weight;     // 1.0 / n_lights (hittable_list.h:45), host-computed
     int32_t n_entries, n_lights, world_bvh_root, render_type, background;
     int32_t has_media;
     int32_t n_media;
@@ -665,12 +668,12 @@ RTW_D d3 mixture_generate(const scene& S, const onb& uvw, d3 o, uint32_t& rng) {
     const double sq = __builtin_sqrt(sph ? 1 - z * z : r2);
     const double phi = kTwoPi * r1;
     double sp, cp;
-    sincos(phi, &sp, &cp);
+    sincos_azimuth(phi, sp, cp);
     return local(basis, d3{cp * sq, sp * sq, z});
 }
 
 RTW_D double lights_pdf_value(const scene& S, d3 o, d3 v) {  // hittable_list.h:44-53
-    const double weight = 1.0 / (double)S.n_lights;
+    const double weight = S.light_weight;  // 1.0 / (double)n_lights, computed once on the host
     double sum = 0.0;
     for (int i = 0; i < S.n_lights; ++i) sum += weight * light_pdf_value(S, S.lights[i], o, v);
     return sum;
@@ -700,11 +703,9 @@ RTW_D double pow5(double x) {
     return x5 + e5;
 }
 
-RTW_D double schlick(double cosine, double ref_idx) {  // material.h:44-49
-    double r0 = (1 - ref_idx) / (1 + ref_idx);
-    r0 = r0 * r0;
-    return r0 + (1 - r0) * pow5(1 - cosine);
-}
+// material.h:44-49 with r0 = ((1 - ref_idx) / (1 + ref_idx))^2 precomputed
+// per material on the host (same expression, same rounding)
+RTW_D double schlick_r0(double cosine, double r0) { return r0 + (1 - r0) * pow5(1 - cosine); }
 
 // ------------------------------------------------------------------ camera
 // camera::get_ray camera.h:36-50, random_in_unit_disk :61-69 (y drawn first)

@@ -255,9 +255,19 @@ __global__ __launch_bounds__(kBlock) void k_intersect(scene S, paths_t P, fresh_
 enum { PS_LOOP, PS_LOAD, PS_TRAVERSE, PS_HIT, PS_SAMPLE, PS_PDF, PS_STORE, PS_N };
 #ifdef RTW_PROF
 __device__ unsigned long long g_prof[PS_N];
+__device__ unsigned long long g_cls[2][8];  // [0] lanes per class, [1] waves with the class present
 struct prof_t {
     uint64_t t;
     uint64_t acc[PS_N];
+    uint32_t lanes[8] = {0, 0, 0, 0, 0, 0, 0, 0}, waves[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // segment class of this lane: 0 miss, 1+type material hit, 7 idle
+    __device__ __forceinline__ void classify(int cls) {
+        for (int k = 0; k < 8; ++k) {
+            const unsigned long long m = __ballot(cls == k);
+            lanes[k] += (uint32_t)__popcll(m);
+            waves[k] += m ? 1u : 0u;
+        }
+    }
     __device__ prof_t() : t(clock64()) {
         for (int k = 0; k < PS_N; ++k) acc[k] = 0;
     }
@@ -267,6 +277,11 @@ struct prof_t {
         t = now;
     }
     __device__ void flush() {
+        if ((threadIdx.x & 63) == 0)
+            for (int k = 0; k < 8; ++k) {
+                atomicAdd(&g_cls[0][k], (unsigned long long)lanes[k]);
+                atomicAdd(&g_cls[1][k], (unsigned long long)waves[k]);
+            }
         for (int k = 0; k < PS_N; ++k) {
             unsigned long long v = acc[k];
             for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
@@ -276,11 +291,13 @@ struct prof_t {
 };
 #elif defined(RTW_REGIONS)  // static attribution: region markers in the ISA
 struct prof_t {
+    __device__ __forceinline__ void classify(int) {}
     __device__ __forceinline__ void mark(int k) { asm volatile(";RTW_REGION %0" ::"i"(k)); }
     __device__ __forceinline__ void flush() {}
 };
 #else
 struct prof_t {
+    __device__ __forceinline__ void classify(int) {}
     __device__ __forceinline__ void mark(int) {}
     __device__ __forceinline__ void flush() {}
 };
@@ -352,12 +369,12 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
             cosine = __builtin_sqrt(1 - ri * ri * (1 - cosine * cosine));
         } else {
             outward = n;
-            ni_over_nt = 1.0 / ri;
+            ni_over_nt = S.mat_aux[2 * mat];  // 1.0 / ri, host-computed
             cosine = -dot(r.d, n) / len(r.d);
         }
         const d3 reflected = reflect(r.d, n);
         d3 refracted{0, 0, 0};
-        const double reflect_prob = refract(r.d, outward, ni_over_nt, refracted) ? schlick(cosine, ri) : 1.0;
+        const double reflect_prob = refract(r.d, outward, ni_over_nt, refracted) ? schlick_r0(cosine, S.mat_aux[2 * mat + 1]) : 1.0;
         dir = (rnd01(rng) < reflect_prob) ? reflected : refracted;
         f = d3{1.0, 1.0, 1.0};
     } else if ((M & SF_ISO) && m.type == RTW_MAT_ISOTROPIC) {  // material.h:257-262
@@ -448,6 +465,7 @@ __device__ __forceinline__ scene lds_scene(const scene& S, const char* base, con
     L.perm = (const int32_t*)rb(S.perm);
     L.media = (const int32_t*)rb(S.media);
     L.prim_onb = (const double*)rb(S.prim_onb);
+    L.mat_aux = (const double*)rb(S.mat_aux);
     return L;
 }
 
@@ -647,6 +665,11 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
             const hit_state h = world_closest<F>(S, x.r, x.rng);
             pf.mark(PS_TRAVERSE);
             ++segs;
+#ifdef RTW_PROF
+            pf.classify(h.prim == -1 ? 0
+                        : 1 + SS.materials[h.prim <= -2 ? SS.entries[-h.prim - 2].phase_material
+                                                        : SS.prims[h.prim].material].type);
+#endif
             d3 E, f;
             const int out = shade_core<M>(SS, x, h.t, h.prim, E, f, pf);
             const d3 thr{s_thr[0][threadIdx.x], s_thr[1][threadIdx.x], s_thr[2][threadIdx.x]};
@@ -972,8 +995,17 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         f[3] = b.v.x, f[4] = b.v.y, f[5] = b.v.z;
         f[6] = b.w.x, f[7] = b.w.y, f[8] = b.w.z;
     }
+    // per material: 1/ref_idx and schlick's r0^2 (material.h:158, :46-47)
+    std::vector<double> mat_aux((size_t)d->n_materials * 2, 0.0);
+    for (int k = 0; k < d->n_materials; ++k) {
+        const double ri = d->materials[k].ref_idx;
+        double r0 = (1 - ri) / (1 + ri);
+        r0 = r0 * r0;
+        mat_aux[2 * k] = 1.0 / ri;
+        mat_aux[2 * k + 1] = r0;
+    }
     std::vector<part> parts = {
-        // parts 0..8 are what shading reads; they come first so a small
+        // parts 0..9 are what shading reads; they come first so a small
         // scene's shading data is one contiguous prefix the shade kernel can
         // stage in LDS
         {d->prims, sizeof(rtw_prim) * d->n_prims, 0},
@@ -985,6 +1017,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {d->has_perlin ? d->perlin_perm : nullptr, d->has_perlin ? sizeof(int32_t) * 768 : 0, 0},
         {media.data(), sizeof(int32_t) * media.size(), 0},
         {frames.data(), sizeof(double) * frames.size(), 0},
+        {mat_aux.data(), sizeof(double) * mat_aux.size(), 0},
         {d->bvh_nodes, sizeof(rtw_bvh_node) * d->n_bvh_nodes, 0},
         {d->bvh_items, sizeof(int32_t) * d->n_bvh_items, 0},
     };
@@ -1011,12 +1044,14 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.perm = (const int32_t*)at(6);
     S.media = (const int32_t*)at(7);
     S.prim_onb = (const double*)at(8);
-    S.nodes = (const rtw_bvh_node*)at(9);
-    S.items = (const int32_t*)at(10);
-    h->shade_bytes = (uint32_t)parts[9].off;  // the shading prefix
+    S.mat_aux = (const double*)at(9);
+    S.nodes = (const rtw_bvh_node*)at(10);
+    S.items = (const int32_t*)at(11);
+    h->shade_bytes = (uint32_t)parts[10].off;  // the shading prefix
     h->scene_base = base;
     S.n_entries = d->n_entries;
     S.n_lights = d->n_lights;
+    S.light_weight = d->n_lights > 0 ? 1.0 / (double)d->n_lights : 0.0;
     S.world_bvh_root = d->world_bvh_root;
     S.render_type = d->render_type;
     S.background = d->background;
@@ -1556,6 +1591,22 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         std::fprintf(stderr, "\n");
         std::memset(pr, 0, sizeof pr);
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof pr));
+        unsigned long long cl[2][8];
+        HIPCHK(hipMemcpyFromSymbol(cl, HIP_SYMBOL(g_cls), sizeof cl));
+        static const char* cn[8] = {"miss", "lambertian", "metal", "dielectric", "light", "isotropic", "-", "idle"};
+        std::fprintf(stderr, "[rtw prof] segment classes (lane share / share of wave-iterations where present):");
+        double lt = 0, wt = 0;
+        for (int k = 0; k < 8; ++k) lt += (double)cl[0][k];
+        wt = (double)(cl[1][0] + 0);  // every wave-iteration has some class; use max as the iteration count
+        for (int k = 0; k < 8; ++k) wt = std::max(wt, (double)cl[1][k]);
+        unsigned long long it = 0;
+        for (int k = 0; k < 8; ++k) it = std::max(it, cl[1][k]);
+        std::fprintf(stderr, " (wave-iterations >= %llu)", it);
+        for (int k = 0; k < 8; ++k)
+            if (cl[0][k]) std::fprintf(stderr, " %s %.3f/%.3f", cn[k], cl[0][k] / lt, cl[1][k] / wt);
+        std::fprintf(stderr, "\n");
+        std::memset(cl, 0, sizeof cl);
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_cls), cl, sizeof cl));
     }
 #endif
     // algorithmic traversal bytes: 56 B ray in +

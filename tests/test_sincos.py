@@ -1,0 +1,18 @@
+"""The device's azimuth sincos (rtw_math.h: fdlibm-style reduction and
+kernels, used for the 2*pi*r1 angle of the cosine and sphere-light samplers)
+is within 1 ulp of glibc's sin/cos -- the functions the reference calls --
+over [0, 2*pi], including next to the quadrant boundaries
+(tests/cpp/sincos_check.cpp)."""
+import subprocess
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_sincos_azimuth_within_one_ulp_of_glibc(tmp_path):
+    exe = tmp_path / "sincos_check"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", f"-I{ROOT / 'raytracingweekend_amd' / 'csrc'}",
+                    str(ROOT / "tests" / "cpp" / "sincos_check.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True, check=True).stdout.split()
+    vals = dict(zip(out[0::2], map(float, out[1::2])))
+    assert vals["max_ulp_sin"] <= 1.0 and vals["max_ulp_cos"] <= 1.0, vals
