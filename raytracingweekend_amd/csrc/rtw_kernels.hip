@@ -696,6 +696,168 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
     }
 }
 
+// Persistent form with material regrouping.  A wave pays for every shading
+// branch one of its lanes takes; on Cornell about half the lanes shade
+// lambertian, 30 % dielectric, 20 % emit or miss, and every wave carries all
+// of them.  Here, after each traversal, the block's 256 paths are sorted by
+// what their hit needs (lambertian, dielectric, metal, isotropic, emitter,
+// miss, idle) with a counting sort over wave ballots and moved through LDS
+// to the lane of their rank, so most waves run one branch.  Idle lanes end
+// up together at the top of the block: they take fresh camera samples
+// there, so ray generation also runs nearly lane-full.
+enum { K_LAMB = 0, K_DIEL, K_METAL, K_ISO, K_EMIT, K_MISS, K_IDLE, K_N };
+
+template <int F, int M, bool LDS>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(M))))
+void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
+    extern __shared__ __attribute__((aligned(16))) char s_scene[];
+    __shared__ uint32_t s_kc[kWaves][K_N];  // per wave, lanes per key
+    __shared__ uint32_t s_seg[kWaves];
+    // the exchange: one path per slot (SoA)
+    __shared__ double x_o[3][kBlock], x_d[3][kBlock], x_tm[kBlock], x_th[3][kBlock], x_t[kBlock];
+    __shared__ int32_t x_prim[kBlock];
+    __shared__ uint32_t x_rng[kBlock], x_depth[kBlock], x_q[kBlock];
+    if (LDS) {
+        const uint4* src = reinterpret_cast<const uint4*>(base);
+        uint4* dst = reinterpret_cast<uint4*>(s_scene);
+        for (uint32_t k = threadIdx.x; k < bytes / 16; k += kBlock) dst[k] = src[k];
+        __syncthreads();
+    }
+    const scene SS = LDS ? lds_scene(S, base, s_scene) : S;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int own = blockIdx.x % kQShards;
+    path_st x;
+    x.depth = 0;
+    d3 thr{1.0, 1.0, 1.0};
+    bool open = true;  // wave-uniform: the queue may still hold samples
+    uint32_t segs = 0;
+    for (;;) {
+        // 1. idle lanes take new camera samples (one reservation per wave)
+        {
+            const bool idle = x.depth == 0;
+            const unsigned long long m = __ballot(idle);
+            if (open && m) {
+                const uint32_t want = (uint32_t)__popcll(m);
+                const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+                uint32_t left = want, given = 0, q = 0;
+                bool got = false;
+                for (int a = 0; a < kQShards && left; ++a) {
+                    const int sh = (own + a) % kQShards;
+                    const unsigned long long lim = shard_limit(sh, J.total);
+                    unsigned long long b = ~0ull;
+                    if (lane == 0) {
+                        const bool dry = a > 0 && __hip_atomic_load(&C->qshard[sh].v, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT) >= lim;
+                        if (!dry) b = atomicAdd(&C->qshard[sh].v, (unsigned long long)left);
+                    }
+                    b = __shfl(b, 0, 64);
+                    if (b == ~0ull || b >= lim) continue;
+                    const uint32_t ok = (uint32_t)min((unsigned long long)left, lim - b);
+                    if (idle && rank >= given && rank < given + ok) {
+                        q = (uint32_t)shard_sample(sh, b + (rank - given));
+                        got = true;
+                    }
+                    given += ok;
+                    left -= ok;
+                }
+                if (left) open = false;
+                if (got) {
+                    x.r = camera_sample(J, q, x.rng);
+                    x.q = q;
+                    x.depth = (uint32_t)J.max_depth;
+                    thr = d3{1.0, 1.0, 1.0};
+                }
+            }
+        }
+        // 2. traversal
+        double th = 0.0;
+        int32_t hp = -1;
+        int key = K_IDLE;
+        if (x.depth != 0) {
+            const hit_state h = world_closest<F>(S, x.r, x.rng);
+            ++segs;
+            th = h.t;
+            hp = h.prim;
+            if (hp == -1) {
+                key = K_MISS;
+            } else {
+                const int mat = hp <= -2 ? SS.entries[-hp - 2].phase_material : SS.prims[hp].material;
+                const int ty = SS.materials[mat].type;
+                key = ty == RTW_MAT_LAMBERTIAN ? K_LAMB
+                      : ty == RTW_MAT_DIELECTRIC ? K_DIEL
+                      : ty == RTW_MAT_METAL ? K_METAL
+                      : ty == RTW_MAT_ISOTROPIC ? K_ISO
+                                                : K_EMIT;
+            }
+        }
+        // 3. counting sort of the block's paths by key
+        uint32_t rank_in_wave = 0;
+#pragma unroll
+        for (int k = 0; k < K_N; ++k) {
+            const unsigned long long m = __ballot(key == k);
+            if (key == k) rank_in_wave = (uint32_t)__popcll(m & lanemask_lt());
+            if (lane == 0) s_kc[wave][k] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        uint32_t dst = rank_in_wave, idle_total = 0;
+#pragma unroll
+        for (int k = 0; k < K_N; ++k) {
+            uint32_t tot = 0, before = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) {
+                const uint32_t c = s_kc[w][k];
+                tot += c;
+                before += (w < (int)wave) ? c : 0u;
+            }
+            if (k < key) dst += tot;
+            if (k == key) dst += before;
+            if (k == K_IDLE) idle_total = tot;
+        }
+        if (idle_total == kBlock) break;  // block-uniform: nothing left to trace or take
+        // 4. move every path to the slot of its rank
+        x_o[0][dst] = x.r.o.x, x_o[1][dst] = x.r.o.y, x_o[2][dst] = x.r.o.z;
+        x_d[0][dst] = x.r.d.x, x_d[1][dst] = x.r.d.y, x_d[2][dst] = x.r.d.z;
+        x_tm[dst] = x.r.t;
+        x_th[0][dst] = thr.x, x_th[1][dst] = thr.y, x_th[2][dst] = thr.z;
+        x_t[dst] = th;
+        x_prim[dst] = hp;
+        x_rng[dst] = x.rng;
+        x_depth[dst] = x.depth;
+        x_q[dst] = x.q;
+        __syncthreads();
+        const uint32_t me = threadIdx.x;
+        x.r = ray{d3{x_o[0][me], x_o[1][me], x_o[2][me]}, d3{x_d[0][me], x_d[1][me], x_d[2][me]}, x_tm[me]};
+        thr = d3{x_th[0][me], x_th[1][me], x_th[2][me]};
+        th = x_t[me];
+        hp = x_prim[me];
+        x.rng = x_rng[me];
+        x.depth = x_depth[me];
+        x.q = x_q[me];
+        // 5. shading, now mostly one branch per wave
+        if (x.depth != 0) {
+            prof_t pf;
+            d3 E, f;
+            const int out = shade_core<M>(SS, x, th, hp, E, f, pf);
+            if (out == SEG_CONTINUE) {
+                thr = thr * f;
+            } else {
+                const d3 L = out == SEG_END ? thr * E : d3{0, 0, 0};
+                double* o = J.L + 3 * (size_t)x.q;
+                o[0] = L.x, o[1] = L.y, o[2] = L.z;
+                x.depth = 0;
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_down(segs, off, 64);
+    if (lane == 0) s_seg[wave] = segs;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int k = 0; k < kWaves; ++k) t += s_seg[k];
+        if (t) atomicAdd(&C->segments[blockIdx.x % 8].v, t);
+    }
+}
+
 // Block-wide exclusive prefix sum of one value per thread (blockDim = kBlock).
 __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1126,17 +1288,45 @@ int persist_grid(size_t shm, int cus) {
     return blocks_per_cu * cus;
 }
 
+template <int FF, int MM, bool LL>
+int persist_sort_grid(size_t shm, int cus) {
+    static int blocks_per_cu = 0;
+    if (!blocks_per_cu) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void*>(&k_persist_sort<FF, MM, LL>), kBlock, shm) != hipSuccess || nb <= 0)
+            nb = 2;
+        blocks_per_cu = nb;
+    }
+    return blocks_per_cu * cus;
+}
+
+// The persistent kernels: material-regrouping k_persist_sort by default,
+// plain k_persist with RTW_SORT=0 (A/B and tests).
+template <int FF, int MM, bool LL>
+void launch_pk(int cus, size_t shm, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C, const char* base,
+               uint32_t bytes) {
+    static const bool sorted = [] {
+        const char* e = std::getenv("RTW_SORT");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if (sorted)
+        hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)), dim3(kBlock),
+                           shm, st, S, J, C, base, bytes);
+    else
+        hipLaunchKernelGGL((k_persist<FF, MM, LL>), dim3(persist_grid<FF, MM, LL>(shm, cus)), dim3(kBlock), shm, st,
+                           S, J, C, base, bytes);
+}
+
 bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C,
                     const char* base, uint32_t bytes) {
     const int pick = pick_shade_mask(mask);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
-#define RTW_PER(FF, MM, LL)                                                                                  \
-    if (f == (FF) && pick == (MM) && lds == (LL)) {                                                        \
-        if (!probe)                                                                                         \
-            hipLaunchKernelGGL((k_persist<FF, MM, LL>), dim3(persist_grid<FF, MM, LL>(shm, cus)), dim3(kBlock), shm, \
-                               st, S, J, C, base, bytes);                                                   \
-        return true;                                                                                       \
+#define RTW_PER(FF, MM, LL)                                            \
+    if (f == (FF) && pick == (MM) && lds == (LL)) {                  \
+        if (!probe) launch_pk<FF, MM, LL>(cus, shm, st, S, J, C, base, bytes); \
+        return true;                                                 \
     }
     // specialised: small list scenes whose shading data fit in LDS, and the
     // lambertian / metal / dielectric sets of the Book-1 scene, flat or BVH
@@ -1148,12 +1338,10 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
 #undef RTW_PER
     // general: every material / texture, scene read through the caches, one
     // instantiation per traversal feature set (a world BVH never holds media)
-#define RTW_PER(FF)                                                                                           \
-    if (f == (FF)) {                                                                                        \
-        if (!probe)                                                                                         \
-            hipLaunchKernelGGL((k_persist<FF, SF_ALL, false>), dim3(persist_grid<FF, SF_ALL, false>(0, cus)),  \
-                               dim3(kBlock), 0, st, S, J, C, base, bytes);                                  \
-        return true;                                                                                       \
+#define RTW_PER(FF)                                                     \
+    if (f == (FF)) {                                                  \
+        if (!probe) launch_pk<FF, SF_ALL, false>(cus, 0, st, S, J, C, base, bytes); \
+        return true;                                                  \
     }
     RTW_PER(0)
     RTW_PER(F_MEDIA)

@@ -137,10 +137,12 @@ def test_reference_default_config_matches_committed_render(gpu):
 
 @pytest.mark.parametrize("scene,bvh", [("cornell_box", False), ("random_balls", True), ("dielectric", False)])
 def test_execution_forms_agree(gpu, monkeypatch, scene, bvh):
-    """The persistent kernel (k_persist, default), the wavefront's fused
-    traversal+shading kernel (k_segment; RTW_MODE=wavefront) and its split
-    pair (k_intersect, k_shade; + RTW_SPLIT=1) run the same arithmetic in the
-    same order per sample: bit-identical accumulators and segment counts."""
+    """The persistent kernel with material regrouping (k_persist_sort,
+    default), without it (k_persist; RTW_SORT=0 -- read once per process, so
+    run here in a child), the wavefront's fused traversal+shading kernel
+    (k_segment; RTW_MODE=wavefront) and its split pair (k_intersect, k_shade;
+    + RTW_SPLIT=1) run the same arithmetic in the same order per sample:
+    bit-identical accumulators and segment counts."""
     nx, ny, spp, depth = 40, 30, 4, 50
     sd = gpu.SceneDesc(scene, nx / ny, use_bvh=bvh)
     ds = gpu.DeviceScene(sd)
@@ -154,6 +156,28 @@ def test_execution_forms_agree(gpu, monkeypatch, scene, bvh):
         ds.close()
     assert sa["segments"] == sb["segments"] == sc["segments"]
     assert np.array_equal(a, b) and np.array_equal(a, c)
+    d = _render_in_child({"RTW_SORT": "0"}, scene, nx, ny, spp, depth, 5, bvh)
+    assert np.array_equal(a, d)
+
+
+def _render_in_child(env, scene, nx, ny, spp, depth, seed, bvh):
+    """Render in a fresh process with extra environment (for switches the
+    library reads once per process)."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / "acc.npy"
+        code = (f"import sys; sys.path.insert(0, {str(root)!r}); import numpy as np; "
+                f"from raytracingweekend_amd import render as r; "
+                f"ds = r.DeviceScene(r.SceneDesc({scene!r}, {nx}/{ny}, use_bvh={bvh})); "
+                f"a, _ = ds.render_accumulate({nx}, {ny}, {spp}, {depth}, seed={seed}); ds.close(); "
+                f"np.save({str(out)!r}, a)")
+        subprocess.run([sys.executable, "-c", code], env={**os.environ, **env}, check=True, timeout=300)
+        return np.load(out)
 
 
 def test_device_finalize_matches_host(gpu):
