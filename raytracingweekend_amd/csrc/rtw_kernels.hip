@@ -1301,14 +1301,18 @@ int persist_sort_grid(size_t shm, int cus) {
     return blocks_per_cu * cus;
 }
 
-// The persistent kernels: material-regrouping k_persist_sort by default,
-// plain k_persist with RTW_SORT=0 (A/B and tests).
+// The persistent kernels: material-regrouping k_persist_sort for list
+// traversal, plain k_persist under a BVH (measured, 1 MI355X: Cornell +14 %,
+// random_balls flat +12 %, Book-2 flat +37 % with regrouping; random_balls
+// BVH -8 %, Book-2 BVH -2 %: divergent BVH walks dominate there and the
+// per-iteration block barriers cost).  RTW_SORT=0/1 forces either (A/B, tests).
 template <int FF, int MM, bool LL>
 void launch_pk(int cus, size_t shm, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C, const char* base,
                uint32_t bytes) {
     static const bool sorted = [] {
         const char* e = std::getenv("RTW_SORT");
-        return !(e && std::atoi(e) == 0);
+        if (e && *e) return std::atoi(e) != 0;
+        return (FF & (F_WBVH | F_GBVH)) == 0;
     }();
     if (sorted)
         hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)), dim3(kBlock),
