@@ -137,9 +137,9 @@ def test_reference_default_config_matches_committed_render(gpu):
 
 @pytest.mark.parametrize("scene,bvh", [("cornell_box", False), ("random_balls", True), ("dielectric", False)])
 def test_execution_forms_agree(gpu, monkeypatch, scene, bvh):
-    """The persistent kernel with material regrouping (k_persist_sort,
-    default), without it (k_persist; RTW_SORT=0 -- read once per process, so
-    run here in a child), the wavefront's fused traversal+shading kernel
+    """The persistent kernel with material regrouping (k_persist_sort) and
+    without it (k_persist) -- RTW_SORT=1/0, read once per process, so run in
+    child processes -- the wavefront's fused traversal+shading kernel
     (k_segment; RTW_MODE=wavefront) and its split pair (k_intersect, k_shade;
     + RTW_SPLIT=1) run the same arithmetic in the same order per sample:
     bit-identical accumulators and segment counts."""
@@ -156,8 +156,9 @@ def test_execution_forms_agree(gpu, monkeypatch, scene, bvh):
         ds.close()
     assert sa["segments"] == sb["segments"] == sc["segments"]
     assert np.array_equal(a, b) and np.array_equal(a, c)
-    d = _render_in_child({"RTW_SORT": "0"}, scene, nx, ny, spp, depth, 5, bvh)
-    assert np.array_equal(a, d)
+    for sort in ("0", "1"):
+        d = _render_in_child({"RTW_SORT": sort}, scene, nx, ny, spp, depth, 5, bvh)
+        assert np.array_equal(a, d), f"RTW_SORT={sort}"
 
 
 def _render_in_child(env, scene, nx, ny, spp, depth, seed, bvh):
