@@ -168,8 +168,10 @@ def main():
     launches = sum(s["launches_intersect"] for s in stats)
     algo = sum(s["bytes_intersect"] for s in stats)
     mode = os.environ.get("RTW_MODE", "persistent")
+    sort_env = os.environ.get("RTW_SORT", "")
+    sorted_pk = sort_env == "1" or (sort_env != "0" and not args.bvh)  # the library's default (launch_pk)
     kernel = ("k_intersect" if os.environ.get("RTW_SPLIT") == "1" else "k_segment") if mode == "wavefront" \
-        else "k_persist"
+        else ("k_persist_sort" if sorted_pk else "k_persist")
     if world > 1:
         v = torch.tensor([seg, ms_isect, launches, algo], dtype=torch.float64, device=dev)
         dist.all_reduce(v)
