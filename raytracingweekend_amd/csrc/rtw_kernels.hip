@@ -1465,7 +1465,7 @@ size_t pass_budget_samples() {
         const long long v = std::atoll(s);
         if (v > 0) return (size_t)v;
     }
-    return size_t(1) << 28;  // 6 GiB of fp64 radiance planes per pass
+    return size_t(1) << 30;  // 24 GiB of per-sample radiance records per pass (T: one pass)
 }
 
 }  // namespace
