@@ -395,56 +395,72 @@ RTW_D bool slab(const rtw_bvh_node& nd, const d3& o, const d3& inv, double t0, d
     return lo <= hi;
 }
 
+// BVH traversal stacks.  A private array (scratch memory) by default; the
+// persistent kernels give each lane a column of an LDS array instead (one
+// bank per lane, no scratch round trips).  Nested walks (a group BVH inside
+// a world-BVH leaf) share one stack above the outer walk's entries; the host
+// checks at upload that the deepest nesting fits (rtw_scene_upload).
 constexpr int kStack = 48;
+constexpr int kLdsStack = 16;
+struct local_stack {
+    static constexpr int cap = kStack;
+    int s[kStack];
+    RTW_D int& at(int i) { return s[i]; }
+};
+struct lds_stack {
+    static constexpr int cap = kLdsStack;
+    int* p;  // &column[0][lane]; entry i at p[i * 256]
+    RTW_D int& at(int i) { return p[i * 256]; }
+};
 
 RTW_D double widen_lo(double t) { return t > 0 ? t * 0.5 : t * 2.0 - 1e-9; }
 RTW_D double widen_hi(double t) { return t * (1 + 1e-12) + 1e-9; }
 
 // BVH over the prims of one group (items = prim indices).
-RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_state& h) {
+template <class STK>
+RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_state& h, STK& stk, int base) {
     const d3 inv = d3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
-    int stack[kStack];
-    int sp = 0;
-    stack[sp++] = root;
-    while (sp > 0) {
-        const rtw_bvh_node nd = S.nodes[stack[--sp]];
+    int sp = base;
+    stk.at(sp++) = root;
+    while (sp > base) {
+        const rtw_bvh_node nd = S.nodes[stk.at(--sp)];
         if (!slab(nd, r.o, inv, widen_lo(t_min), widen_hi(h.t))) continue;
         if (nd.count > 0) {
             for (int k = 0; k < nd.count; ++k) arbitrate(S, S.items[nd.left + k], r, t_min, h);
-        } else if (sp + 2 <= kStack) {
-            stack[sp++] = nd.right;
-            stack[sp++] = nd.left;
+        } else if (sp + 2 <= STK::cap) {  // always true: depth checked at upload
+            stk.at(sp++) = nd.right;
+            stk.at(sp++) = nd.left;
         }
     }
 }
 
-template <int F>
-RTW_D void group_closest(const scene& S, const entry_v& e, const ray& r, double t_min, hit_state& h) {
+template <int F, class STK>
+RTW_D void group_closest(const scene& S, const entry_v& e, const ray& r, double t_min, hit_state& h, STK& stk) {
     if ((F & F_GBVH) && e.bvh_root >= 0)
-        group_bvh(S, e.bvh_root, r, t_min, h);
+        group_bvh(S, e.bvh_root, r, t_min, h, stk, 0);
     else
         group_scan(S, e.first_prim, e.n_prims, r, t_min, h);
 }
 
 // Closest t of a medium's boundary in (t0, t1) (hittable.h:438-449); the
 // boundary is the entry's ops + group.
-template <int F>
-RTW_D bool boundary_t(const scene& S, const entry_v& e, const ray& r, double t0, double t1, double& t) {
+template <int F, class STK>
+RTW_D bool boundary_t(const scene& S, const entry_v& e, const ray& r, double t0, double t1, double& t, STK& stk) {
     const ray lr = entry_local_ray<true>(e, r);
     hit_state h{t1, -1, false};
-    group_closest<F>(S, e, lr, t0, h);
+    group_closest<F>(S, e, lr, t0, h, stk);
     if (h.prim == -1) return false;
     t = h.t;
     return true;
 }
 
 // constant_medium::hit hittable.h:430-479 (at most one draw per call)
-template <int F>
+template <int F, class STK>
 RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& r, double t_min, double t_max, uint32_t& rng,
-                    double& t_out) {
+                    double& t_out, STK& stk) {
     double t1, t2;
-    if (!boundary_t<F>(S, e, r, -kDblMax, kDblMax, t1)) return false;
-    if (!boundary_t<F>(S, e, r, t1 + kStep, kDblMax, t2)) return false;
+    if (!boundary_t<F>(S, e, r, -kDblMax, kDblMax, t1, stk)) return false;
+    if (!boundary_t<F>(S, e, r, t1 + kStep, kDblMax, t2, stk)) return false;
     if (t1 < t_min) t1 = t_min;
     if (t2 > t_max) t2 = t_max;
     if (t1 >= t2) return false;
@@ -464,30 +480,29 @@ RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& r, double t_min
 // primitive is deterministic; the second walk re-accepts only what the first
 // kept).  With media, the second walk can only change the result through the
 // media's fresh draws, so it re-evaluates just the media, in list order.
-template <int F>
-RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
+template <int F, class STK>
+RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& stk) {
     hit_state h{kDblMax, -1, false};
     if constexpr ((F & F_WBVH) != 0 && (F & F_MEDIA) == 0) {
         const d3 inv = d3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
-        int stack[kStack];
         int sp = 0;
-        stack[sp++] = S.world_bvh_root;
+        stk.at(sp++) = S.world_bvh_root;
         while (sp > 0) {
-            const rtw_bvh_node nd = S.nodes[stack[--sp]];
+            const rtw_bvh_node nd = S.nodes[stk.at(--sp)];
             if (!slab(nd, r.o, inv, widen_lo(kTMin), widen_hi(h.t))) continue;
             if (nd.count > 0) {
                 for (int k = 0; k < nd.count; ++k) {
                     const entry_v e = view_entry<false>(S.entries, S.items[nd.left + k]);
                     const ray lr = entry_local_ray<false>(e, r);
                     if ((F & F_GBVH) && e.bvh_root >= 0) {
-                        group_bvh(S, e.bvh_root, lr, kTMin, h);
+                        group_bvh(S, e.bvh_root, lr, kTMin, h, stk, sp);
                     } else {
                         for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMin, h);
                     }
                 }
-            } else if (sp + 2 <= kStack) {
-                stack[sp++] = nd.right;
-                stack[sp++] = nd.left;
+            } else if (sp + 2 <= STK::cap) {  // always true: depth checked at upload
+                stk.at(sp++) = nd.right;
+                stk.at(sp++) = nd.left;
             }
         }
         return h;
@@ -496,7 +511,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
             const entry_v e = view_entry<true>(S.entries, ei);
             if ((F & F_MEDIA) && e.kind == RTW_ENTRY_MEDIUM) {
                 double t;
-                if (medium_t<F>(S, e, r, kTMin, h.t, rng, t)) {
+                if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk)) {
                     h.t = t;
                     h.prim = -(2 + ei);
                     h.rect = false;
@@ -504,14 +519,14 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
                 continue;
             }
             const ray lr = entry_local_ray<true>(e, r);
-            group_closest<F>(S, e, lr, kTMin, h);
+            group_closest<F>(S, e, lr, kTMin, h, stk);
         }
         if (F & F_MEDIA) {
             for (int k = 0; k < S.n_media; ++k) {
                 const int ei = ld(&S.media[k]);
                 const entry_v e = view_entry<true>(S.entries, ei);
                 double t;
-                if (medium_t<F>(S, e, r, kTMin, h.t, rng, t)) {
+                if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk)) {
                     h.t = t;
                     h.prim = -(2 + ei);
                     h.rect = false;
@@ -520,6 +535,11 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
         }
         return h;
     }
+}
+template <int F>
+RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
+    local_stack stk;
+    return world_closest<F>(S, r, rng, stk);
 }
 
 // Reconstruct the hit record (p, normal, material) of a winner exactly as

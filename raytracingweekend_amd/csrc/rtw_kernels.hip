@@ -580,13 +580,15 @@ struct ray_batch {  // one wave's buffer of generated camera samples (LDS)
 #else
 #define RTW_PERSIST_WAVES(M) 4
 #endif
-template <int F, int M, bool LDS>
+// LST: BVH traversal stacks in LDS (one column per lane) instead of scratch.
+template <int F, int M, bool LDS, bool LST = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(M))))
 void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kWaves];
     __shared__ ray_batch s_batch[kWaves];
     __shared__ double s_thr[3][kBlock];  // each lane's path throughput
+    __shared__ int s_stack[LST ? kLdsStack : 1][kBlock];
     if (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(base);
         uint4* dst = reinterpret_cast<uint4*>(s_scene);
@@ -662,7 +664,13 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
         if (!__any(x.depth != 0)) break;
         pf.mark(PS_LOAD);
         if (x.depth != 0) {
-            const hit_state h = world_closest<F>(S, x.r, x.rng);
+            hit_state h;
+            if constexpr (LST) {
+                lds_stack stk{&s_stack[0][threadIdx.x]};
+                h = world_closest<F>(S, x.r, x.rng, stk);
+            } else {
+                h = world_closest<F>(S, x.r, x.rng);
+            }
             pf.mark(PS_TRAVERSE);
             ++segs;
 #ifdef RTW_PROF
@@ -1086,6 +1094,7 @@ struct handle_t {
     uint32_t pool_cap = 0;
     int grid = 2048;
     int cus = 256;
+    int stack_need = 0;  // deepest BVH stack a traversal of this scene can use
     std::vector<hipEvent_t> events;
 };
 
@@ -1233,6 +1242,29 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         m |= t == RTW_TEX_NOISE ? SF_NOISE : t == RTW_TEX_CHECKER ? SF_CHECKER : 0;
     }
     h->shade_mask = m;
+    // BVH stack depth: a walk pushes two children per inner node and pops
+    // one, so it holds at most depth + 1 entries; a group BVH inside a world
+    // leaf stacks on top of the world walk
+    auto depth = [&](int root) {
+        int best = 0;
+        std::vector<std::pair<int, int>> todo{{root, 1}};
+        while (!todo.empty()) {
+            const auto [n, dd] = todo.back();
+            todo.pop_back();
+            best = std::max(best, dd);
+            const rtw_bvh_node& N = d->bvh_nodes[n];
+            if (N.count == 0) todo.push_back({N.left, dd + 1}), todo.push_back({N.right, dd + 1});
+        }
+        return best;
+    };
+    int group_depth = 0;
+    for (int e = 0; e < d->n_entries; ++e)
+        if (d->entries[e].bvh_root >= 0) group_depth = std::max(group_depth, depth(d->entries[e].bvh_root));
+    const int world_depth = d->world_bvh_root >= 0 ? depth(d->world_bvh_root) : 0;
+    h->stack_need = world_depth + group_depth + 2;
+    if (h->stack_need > kStack)
+        return rtw_fail(RTW_ERR_UNSUPPORTED, "BVH too deep for the traversal stack (" + std::to_string(h->stack_need) +
+                                                 " > " + std::to_string(kStack) + " entries)");
     return RTW_OK;
 }
 
@@ -1275,13 +1307,13 @@ bool launch_segment(bool probe, int f, int mask, int grid, hipStream_t st, const
 // Persistent kernel for the same instantiation set.  grid 0 = probe only.
 // The grid is the number of blocks that can be resident at once (occupancy
 // query per instantiation, cached), so every block starts immediately.
-template <int FF, int MM, bool LL>
+template <int FF, int MM, bool LL, bool LST>
 int persist_grid(size_t shm, int cus) {
     static int blocks_per_cu = 0;
     if (!blocks_per_cu) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_persist<FF, MM, LL>),
-                                                         kBlock, shm) != hipSuccess || nb <= 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void*>(&k_persist<FF, MM, LL, LST>), kBlock, shm) != hipSuccess || nb <= 0)
             nb = 2;
         blocks_per_cu = nb;
     }
@@ -1308,7 +1340,7 @@ int persist_sort_grid(size_t shm, int cus) {
 // per-iteration block barriers cost).  RTW_SORT=0/1 forces either (A/B, tests).
 template <int FF, int MM, bool LL>
 void launch_pk(int cus, size_t shm, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C, const char* base,
-               uint32_t bytes) {
+               uint32_t bytes, int stack_need) {
     static const bool sorted = [] {
         const char* e = std::getenv("RTW_SORT");
         if (e && *e) return std::atoi(e) != 0;
@@ -1317,19 +1349,22 @@ void launch_pk(int cus, size_t shm, hipStream_t st, const scene& S, const job_t&
     if (sorted)
         hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)), dim3(kBlock),
                            shm, st, S, J, C, base, bytes);
+    else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack)
+        hipLaunchKernelGGL((k_persist<FF, MM, LL, true>), dim3(persist_grid<FF, MM, LL, true>(shm, cus)),
+                           dim3(kBlock), shm, st, S, J, C, base, bytes);
     else
-        hipLaunchKernelGGL((k_persist<FF, MM, LL>), dim3(persist_grid<FF, MM, LL>(shm, cus)), dim3(kBlock), shm, st,
-                           S, J, C, base, bytes);
+        hipLaunchKernelGGL((k_persist<FF, MM, LL, false>), dim3(persist_grid<FF, MM, LL, false>(shm, cus)),
+                           dim3(kBlock), shm, st, S, J, C, base, bytes);
 }
 
 bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C,
-                    const char* base, uint32_t bytes) {
+                    const char* base, uint32_t bytes, int stack_need = kStack) {
     const int pick = pick_shade_mask(mask);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
 #define RTW_PER(FF, MM, LL)                                            \
     if (f == (FF) && pick == (MM) && lds == (LL)) {                  \
-        if (!probe) launch_pk<FF, MM, LL>(cus, shm, st, S, J, C, base, bytes); \
+        if (!probe) launch_pk<FF, MM, LL>(cus, shm, st, S, J, C, base, bytes, stack_need); \
         return true;                                                 \
     }
     // specialised: small list scenes whose shading data fit in LDS, and the
@@ -1344,7 +1379,7 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     // instantiation per traversal feature set (a world BVH never holds media)
 #define RTW_PER(FF)                                                     \
     if (f == (FF)) {                                                  \
-        if (!probe) launch_pk<FF, SF_ALL, false>(cus, 0, st, S, J, C, base, bytes); \
+        if (!probe) launch_pk<FF, SF_ALL, false>(cus, 0, st, S, J, C, base, bytes, stack_need); \
         return true;                                                  \
     }
     RTW_PER(0)
@@ -1647,7 +1682,8 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
                 HIPCHK(hipEventRecord(h->events[e0], st));
             }
-            launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base, h->shade_bytes);
+            launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base, h->shade_bytes,
+                           h->stack_need);
             HIPCHK(hipGetLastError());
             if (timed) {
                 HIPCHK(hipEventRecord(h->events[e1], st));
