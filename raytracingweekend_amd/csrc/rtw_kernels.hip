@@ -739,6 +739,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
     d3 thr{1.0, 1.0, 1.0};
     bool open = true;  // wave-uniform: the queue may still hold samples
     uint32_t segs = 0;
+    prof_t pk;  // section profiler (RTW_PROF builds): refill, traverse, sort, exchange, shade
     for (;;) {
         // 1. idle lanes take new camera samples (one reservation per wave)
         {
@@ -777,6 +778,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
                 }
             }
         }
+        pk.mark(PS_LOAD);
         // 2. traversal
         double th = 0.0;
         int32_t hp = -1;
@@ -798,6 +800,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
                                                 : K_EMIT;
             }
         }
+        pk.mark(PS_TRAVERSE);
         // 3. counting sort of the block's paths by key
         uint32_t rank_in_wave = 0;
 #pragma unroll
@@ -822,6 +825,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
             if (k == K_IDLE) idle_total = tot;
         }
         if (idle_total == kBlock) break;  // block-uniform: nothing left to trace or take
+        pk.mark(PS_HIT);
         // 4. move every path to the slot of its rank
         x_o[0][dst] = x.r.o.x, x_o[1][dst] = x.r.o.y, x_o[2][dst] = x.r.o.z;
         x_d[0][dst] = x.r.d.x, x_d[1][dst] = x.r.d.y, x_d[2][dst] = x.r.d.z;
@@ -841,6 +845,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         x.rng = x_rng[me];
         x.depth = x_depth[me];
         x.q = x_q[me];
+        pk.mark(PS_SAMPLE);
         // 5. shading, now mostly one branch per wave
         if (x.depth != 0) {
             prof_t pf;
@@ -855,7 +860,9 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
                 x.depth = 0;
             }
         }
+        pk.mark(PS_STORE);
     }
+    pk.flush();
     for (int off = 32; off > 0; off >>= 1) segs += __shfl_down(segs, off, 64);
     if (lane == 0) s_seg[wave] = segs;
     __syncthreads();
