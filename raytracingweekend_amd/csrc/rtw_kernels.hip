@@ -715,20 +715,25 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
 // there, so ray generation also runs nearly lane-full.
 enum { K_LAMB = 0, K_DIEL, K_METAL, K_ISO, K_EMIT, K_MISS, K_IDLE, K_N };
 
+#ifndef RTW_SORT_BLOCK
+#define RTW_SORT_BLOCK 256
+#endif
+constexpr int kSortBlock = RTW_SORT_BLOCK;  // paths regrouped together (one workgroup)
+constexpr int kSortWaves = kSortBlock / 64;
 template <int F, int M, bool LDS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(M))))
+__global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(M))))
 void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
-    __shared__ uint32_t s_kc[kWaves][K_N];  // per wave, lanes per key
-    __shared__ uint32_t s_seg[kWaves];
+    __shared__ uint32_t s_kc[kSortWaves][K_N];  // per wave, lanes per key
+    __shared__ uint32_t s_seg[kSortWaves];
     // the exchange: one path per slot (SoA)
-    __shared__ double x_o[3][kBlock], x_d[3][kBlock], x_tm[kBlock], x_th[3][kBlock], x_t[kBlock];
-    __shared__ int32_t x_prim[kBlock];
-    __shared__ uint32_t x_rng[kBlock], x_depth[kBlock], x_q[kBlock];
+    __shared__ double x_o[3][kSortBlock], x_d[3][kSortBlock], x_tm[kSortBlock], x_th[3][kSortBlock], x_t[kSortBlock];
+    __shared__ int32_t x_prim[kSortBlock];
+    __shared__ uint32_t x_rng[kSortBlock], x_depth[kSortBlock], x_q[kSortBlock];
     if (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(base);
         uint4* dst = reinterpret_cast<uint4*>(s_scene);
-        for (uint32_t k = threadIdx.x; k < bytes / 16; k += kBlock) dst[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < bytes / 16; k += kSortBlock) dst[k] = src[k];
         __syncthreads();
     }
     const scene SS = LDS ? lds_scene(S, base, s_scene) : S;
@@ -815,7 +820,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         for (int k = 0; k < K_N; ++k) {
             uint32_t tot = 0, before = 0;
 #pragma unroll
-            for (int w = 0; w < kWaves; ++w) {
+            for (int w = 0; w < kSortWaves; ++w) {
                 const uint32_t c = s_kc[w][k];
                 tot += c;
                 before += (w < (int)wave) ? c : 0u;
@@ -824,7 +829,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
             if (k == key) dst += before;
             if (k == K_IDLE) idle_total = tot;
         }
-        if (idle_total == kBlock) break;  // block-uniform: nothing left to trace or take
+        if (idle_total == kSortBlock) break;  // block-uniform: nothing left to trace or take
         pk.mark(PS_HIT);
         // 4. move every path to the slot of its rank
         x_o[0][dst] = x.r.o.x, x_o[1][dst] = x.r.o.y, x_o[2][dst] = x.r.o.z;
@@ -868,7 +873,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
-        for (int k = 0; k < kWaves; ++k) t += s_seg[k];
+        for (int k = 0; k < kSortWaves; ++k) t += s_seg[k];
         if (t) atomicAdd(&C->segments[blockIdx.x % 8].v, t);
     }
 }
@@ -1333,7 +1338,7 @@ int persist_sort_grid(size_t shm, int cus) {
     if (!blocks_per_cu) {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void*>(&k_persist_sort<FF, MM, LL>), kBlock, shm) != hipSuccess || nb <= 0)
+                &nb, reinterpret_cast<const void*>(&k_persist_sort<FF, MM, LL>), kSortBlock, shm) != hipSuccess || nb <= 0)
             nb = 2;
         blocks_per_cu = nb;
     }
@@ -1354,8 +1359,8 @@ void launch_pk(int cus, size_t shm, hipStream_t st, const scene& S, const job_t&
         return (FF & (F_WBVH | F_GBVH)) == 0;
     }();
     if (sorted)
-        hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)), dim3(kBlock),
-                           shm, st, S, J, C, base, bytes);
+        hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)),
+                           dim3(kSortBlock), shm, st, S, J, C, base, bytes);
     else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack)
         hipLaunchKernelGGL((k_persist<FF, MM, LL, true>), dim3(persist_grid<FF, MM, LL, true>(shm, cus)),
                            dim3(kBlock), shm, st, S, J, C, base, bytes);
