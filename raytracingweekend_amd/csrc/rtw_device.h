@@ -137,6 +137,13 @@ RTW_HD onb onb_from_w(d3 n) {  // onb.h:32-38
 RTW_HD d3 local(const onb& b, d3 a) { return b.u * a.x + b.v * a.y + b.w * a.z; }  // onb.h:21-24
 
 // ------------------------------------------------------------------ scene
+// entry >= 0: one world-list entry; WORLD_RUN_PLAIN: consecutive plain
+// entries (one untransformed group each) scanned as their contiguous prims;
+// WORLD_RUN_YSPHERES: the same, all spheres for ysphere_scan.
+enum : int { WORLD_RUN_PLAIN = -1, WORLD_RUN_YSPHERES = -2 };
+struct world_run {
+    int32_t entry, first_prim, n_prims, movers;  // movers: the prims hold DP_MOVING_COMMON*
+};
 struct scene {
     const rtw_prim* prims;
     const rtw_entry* entries;
@@ -154,6 +161,12 @@ struct scene {
     int32_t has_media;
     int32_t n_media;
     const int32_t* media;  // entry indices of media, in list order
+    // World list as runs (world_closest)
+    const world_run* runs;
+    const int32_t* entry_movers;  // per entry: its group holds DP_MOVING_COMMON* spheres
+    int32_t n_runs;
+    int32_t mv_common;     // some prims are DP_MOVING_COMMON*
+    double mv_t0, mv_den;  // their time0 and time1 - time0
 };
 
 // Scene features a traversal kernel is specialised for.
@@ -193,9 +206,10 @@ RTW_D T rd(const T* p) {
 struct entry_v {
     const rtw_entry* p;
     int kind, first_prim, n_prims, n_ops, bvh_root;
+    bool movers;  // the group holds DP_MOVING_COMMON* spheres (scene::entry_movers)
 };
 template <bool U>
-RTW_D entry_v view_entry(const rtw_entry* E, int i) {
+RTW_D entry_v view_entry(const rtw_entry* E, const int32_t* M, int i) {
     entry_v e;
     e.p = E + i;
     e.kind = rd<U>(&E[i].kind);
@@ -203,27 +217,51 @@ RTW_D entry_v view_entry(const rtw_entry* E, int i) {
     e.n_prims = rd<U>(&E[i].n_prims);
     e.n_ops = rd<U>(&E[i].n_ops);
     e.bvh_root = rd<U>(&E[i].bvh_root);
+    e.movers = rd<U>(&M[i]) != 0;
     return e;
 }
 
-RTW_D bool is_sphere(int type) { return type <= RTW_PRIM_MOVING_SPHERE; }
+// Device primitive types.  rtw_scene_upload rewrites the sphere records it
+// copies to the GPU (the caller's rtw_scene_desc is untouched), each value
+// with the reference's own expression, evaluated once instead of per test:
+//   spheres:         p[9] = radius * radius                  (sphere.h:52)
+//   moving spheres:  p[4..6] = center1 - center0, p[8] = time1 - time0
+//                                                             (sphere.h:24)
+// and moving spheres whose (time0, time1) equal the scene's common interval
+// (scene::mv_t0 / mv_den) get DP_MOVING_COMMON: their fraction
+// (time - time0) / (time1 - time0) is computed once per walk (motion_frac)
+// instead of once per sphere.  DP_MOVING_COMMON_Y: in addition
+// center1 - center0 = (0, dy, 0) and center0.x, center0.z are nonzero, so
+// center0.x + 0 * f == center0.x exactly (f is finite: upload checks the
+// interval) and only y moves.
+enum : int { DP_MOVING_COMMON = 5, DP_MOVING_COMMON_Y = 6 };
+RTW_HD bool is_sphere(int type) { return type < RTW_PRIM_RECT_XY || type > RTW_PRIM_RECT_YZ; }
 
-// sphere.h:22-25
-RTW_D d3 sphere_center(const rtw_prim& s, double time) {
+// The moving-sphere fraction (time - time0) / (time1 - time0) of the
+// scene's common interval, computed once per walk over prims that hold
+// DP_MOVING_COMMON* spheres (world_run::movers, scene::entry_movers; the
+// walk's transforms keep the ray's time), else not at all.
+RTW_D double motion_frac(const scene& S, double time, bool movers) {
+    return movers ? (time - S.mv_t0) / S.mv_den : 0.0;
+}
+
+// sphere.h:22-25: center0 + ((time - time0) / (time1 - time0)) * (center1 - center0),
+// fc = motion_frac(...)
+RTW_D d3 sphere_center(const rtw_prim& s, double time, double fc) {
     const d3 c0 = ld3(s.p);
-    if (s.type != RTW_PRIM_MOVING_SPHERE) return c0;
-    const double f = (time - s.p[7]) / (s.p[8] - s.p[7]);
-    return c0 + (ld3(s.p + 4) - c0) * f;
+    if (s.type == RTW_PRIM_SPHERE) return c0;
+    if (s.type == DP_MOVING_COMMON_Y) return d3{c0.x, c0.y + s.p[5] * fc, c0.z};
+    const double f = s.type == DP_MOVING_COMMON ? fc : (time - s.p[7]) / s.p[8];
+    return c0 + ld3(s.p + 4) * f;
 }
 
 // sphere.h:46-81: near root if in (t_min, t_max), else far root.
-RTW_D bool sphere_t(const rtw_prim& s, const ray& r, double t_min, double t_max, double& t_out) {
-    const d3 cc = sphere_center(s, r.t);
-    const double radius = s.p[3];
+RTW_D bool sphere_t(const rtw_prim& s, const ray& r, double t_min, double t_max, double& t_out, double fc) {
+    const d3 cc = sphere_center(s, r.t, fc);
     const d3 oc = r.o - cc;
     const double a = dot(r.d, r.d);
     const double b = dot(oc, r.d);
-    const double c = dot(oc, oc) - radius * radius;
+    const double c = dot(oc, oc) - s.p[9];  // radius * radius
     const double disc = b * b - a * c;
     if (disc > 0) {
         const double sq = __builtin_sqrt(disc);
@@ -262,8 +300,8 @@ RTW_D bool rect_t(const rtw_prim& q, const ray& r, double t0, double t1, double&
     return rect_axis_t<0, 1, 2>(q, r, t0, t1, t_out);
 }
 
-RTW_D bool prim_t(const rtw_prim& q, const ray& r, double t0, double t1, double& t_out) {
-    return is_sphere(q.type) ? sphere_t(q, r, t0, t1, t_out) : rect_t(q, r, t0, t1, t_out);
+RTW_D bool prim_t(const rtw_prim& q, const ray& r, double t0, double t1, double& t_out, double fc) {
+    return is_sphere(q.type) ? sphere_t(q, r, t0, t1, t_out, fc) : rect_t(q, r, t0, t1, t_out);
 }
 
 RTW_HD d3 rect_normal(int type) {
@@ -340,15 +378,78 @@ struct hit_state {
 // Linear closest hit over prims [first, first+n) of one group, in list order
 // (t range (t_min, closest]) with the reference's own comparisons; the
 // primitive data are wave-uniform scalar loads.
-RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h) {
+RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, bool movers) {
+    const double fc = motion_frac(S, r.t, movers);
+    const double a = dot(r.d, r.d);  // sphere.h:50, the same for every sphere
     for (int i = 0; i < n; ++i) {
         const rtw_prim q = uprim(S.prims, first + i);
-        double t;
-        if (prim_t(q, r, t_min, h.t, t)) {
-            h.t = t;
-            h.prim = first + i;
-            h.rect = !is_sphere(q.type);
+        if (is_sphere(q.type)) {
+            // sphere_t inlined so the winner is written where it is found
+            // (no per-prim merge of the running best on the common miss path)
+            const d3 oc = r.o - sphere_center(q, r.t, fc);
+            const double b = dot(oc, r.d);
+            const double c = dot(oc, oc) - q.p[9];
+            const double disc = b * b - a * c;
+            if (disc > 0) {
+                const double sq = __builtin_sqrt(disc);
+                double temp = (-b - sq) / a;
+                bool ok = temp < h.t && temp > t_min;
+                if (!ok) {
+                    temp = (-b + sq) / a;
+                    ok = temp < h.t && temp > t_min;
+                }
+                if (ok) {
+                    h.t = temp;
+                    h.prim = first + i;
+                    h.rect = false;
+                }
+            }
+        } else {
+            double t;
+            if (rect_t(q, r, t_min, h.t, t)) {
+                h.t = t;
+                h.prim = first + i;
+                h.rect = true;
+            }
         }
+    }
+}
+
+// group_scan for a run of spheres that all move along y only (or not at
+// all): centre (c0.x, c0.y + p[5] * fc, c0.z).  The upload forms such runs
+// (WORLD_RUN_YSPHERES) from DP_MOVING_COMMON_Y spheres and static spheres
+// with c0.y != 0, whose p[5] it sets to 0 (c0.y + 0 * fc == c0.y exactly,
+// fc finite), so one branch-free body serves the whole run: the Book-1
+// random_balls list.  Same arithmetic as sphere.h:46-81 per sphere.
+RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, double fc) {
+    const double a = dot(r.d, r.d);
+    // software-pipelined scalar loads: sphere i+1's record is requested
+    // before sphere i is tested, so the scalar-cache latency hides behind
+    // the test instead of stalling every iteration
+    const double* p = S.prims[first].p;
+    double cx = ld(p), cy = ld(p + 1), cz = ld(p + 2), dy = ld(p + 5), rr = ld(p + 9);
+    for (int i = 0; i < n; ++i) {
+        const double* pn = S.prims[first + (i + 1 < n ? i + 1 : i)].p;
+        const double nx = ld(pn), ny = ld(pn + 1), nz = ld(pn + 2), ndy = ld(pn + 5), nrr = ld(pn + 9);
+        const d3 oc{r.o.x - cx, r.o.y - (cy + dy * fc), r.o.z - cz};
+        const double b = dot(oc, r.d);
+        const double c = dot(oc, oc) - rr;
+        const double disc = b * b - a * c;
+        if (disc > 0) {
+            const double sq = __builtin_sqrt(disc);
+            double temp = (-b - sq) / a;
+            bool ok = temp < h.t && temp > t_min;
+            if (!ok) {
+                temp = (-b + sq) / a;
+                ok = temp < h.t && temp > t_min;
+            }
+            if (ok) {
+                h.t = temp;
+                h.prim = first + i;
+                h.rect = false;
+            }
+        }
+        cx = nx, cy = ny, cz = nz, dy = ndy, rr = nrr;
     }
 }
 
@@ -357,14 +458,14 @@ RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_m
 // arbitrated by better().  A sphere is probed with an open upper bound so an
 // exact tie reaches the arbiter; its root choice is unchanged (if the near root
 // lies beyond h.t so does the far one).
-RTW_D void arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_state& h) {
+RTW_D void arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_state& h, double fc) {
     const rtw_prim q = S.prims[pi];
     const bool rl = !is_sphere(q.type);
     double t;
     if (rl) {
         if (!rect_t(q, r, t_min, h.t, t)) return;
     } else {
-        if (!sphere_t(q, r, t_min, kDblMax, t) || t > h.t) return;
+        if (!sphere_t(q, r, t_min, kDblMax, t, fc) || t > h.t) return;
     }
     if (better(t, pi, rl, h.t, h.prim, h.rect, h.prim != -1)) {
         h.t = t;
@@ -418,7 +519,9 @@ RTW_D double widen_hi(double t) { return t * (1 + 1e-12) + 1e-9; }
 
 // BVH over the prims of one group (items = prim indices).
 template <class STK>
-RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_state& h, STK& stk, int base) {
+RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_state& h, STK& stk, int base,
+                     bool movers) {
+    const double fc = motion_frac(S, r.t, movers);
     const d3 inv = d3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
     int sp = base;
     stk.at(sp++) = root;
@@ -426,7 +529,7 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
         const rtw_bvh_node nd = S.nodes[stk.at(--sp)];
         if (!slab(nd, r.o, inv, widen_lo(t_min), widen_hi(h.t))) continue;
         if (nd.count > 0) {
-            for (int k = 0; k < nd.count; ++k) arbitrate(S, S.items[nd.left + k], r, t_min, h);
+            for (int k = 0; k < nd.count; ++k) arbitrate(S, S.items[nd.left + k], r, t_min, h, fc);
         } else if (sp + 2 <= STK::cap) {  // always true: depth checked at upload
             stk.at(sp++) = nd.right;
             stk.at(sp++) = nd.left;
@@ -437,9 +540,9 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
 template <int F, class STK>
 RTW_D void group_closest(const scene& S, const entry_v& e, const ray& r, double t_min, hit_state& h, STK& stk) {
     if ((F & F_GBVH) && e.bvh_root >= 0)
-        group_bvh(S, e.bvh_root, r, t_min, h, stk, 0);
+        group_bvh(S, e.bvh_root, r, t_min, h, stk, 0, e.movers);
     else
-        group_scan(S, e.first_prim, e.n_prims, r, t_min, h);
+        group_scan(S, e.first_prim, e.n_prims, r, t_min, h, e.movers);
 }
 
 // Closest t of a medium's boundary in (t0, t1) (hittable.h:438-449); the
@@ -484,6 +587,7 @@ template <int F, class STK>
 RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& stk) {
     hit_state h{kDblMax, -1, false};
     if constexpr ((F & F_WBVH) != 0 && (F & F_MEDIA) == 0) {
+        const double fc = motion_frac(S, r.t, S.mv_common != 0);  // transforms keep the ray's time
         const d3 inv = d3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
         int sp = 0;
         stk.at(sp++) = S.world_bvh_root;
@@ -492,12 +596,12 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             if (!slab(nd, r.o, inv, widen_lo(kTMin), widen_hi(h.t))) continue;
             if (nd.count > 0) {
                 for (int k = 0; k < nd.count; ++k) {
-                    const entry_v e = view_entry<false>(S.entries, S.items[nd.left + k]);
+                    const entry_v e = view_entry<false>(S.entries, S.entry_movers, S.items[nd.left + k]);
                     const ray lr = entry_local_ray<false>(e, r);
                     if ((F & F_GBVH) && e.bvh_root >= 0) {
-                        group_bvh(S, e.bvh_root, lr, kTMin, h, stk, sp);
+                        group_bvh(S, e.bvh_root, lr, kTMin, h, stk, sp, S.mv_common != 0);
                     } else {
-                        for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMin, h);
+                        for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMin, h, fc);
                     }
                 }
             } else if (sp + 2 <= STK::cap) {  // always true: depth checked at upload
@@ -507,24 +611,48 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
         }
         return h;
     } else {
-        for (int ei = 0; ei < S.n_entries; ++ei) {
-            const entry_v e = view_entry<true>(S.entries, ei);
-            if ((F & F_MEDIA) && e.kind == RTW_ENTRY_MEDIUM) {
-                double t;
-                if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk)) {
-                    h.t = t;
-                    h.prim = -(2 + ei);
-                    h.rect = false;
+        if constexpr ((F & F_MEDIA) != 0) {
+            // entry by entry: with media the run form spills more registers
+            // than it saves (measured, Book-2 BVH)
+            for (int ei = 0; ei < S.n_entries; ++ei) {
+                const entry_v e = view_entry<true>(S.entries, S.entry_movers, ei);
+                if (e.kind == RTW_ENTRY_MEDIUM) {
+                    double t;
+                    if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk)) {
+                        h.t = t;
+                        h.prim = -(2 + ei);
+                        h.rect = false;
+                    }
+                    continue;
                 }
-                continue;
+                const ray lr = entry_local_ray<true>(e, r);
+                group_closest<F>(S, e, lr, kTMin, h, stk);
             }
-            const ray lr = entry_local_ray<true>(e, r);
-            group_closest<F>(S, e, lr, kTMin, h, stk);
+        } else {
+            for (int ri = 0; ri < S.n_runs; ++ri) {
+                // one scan site for plain runs and transformed groups alike
+                const int ei = ld(&S.runs[ri].entry);
+                if (ei == WORLD_RUN_YSPHERES) {
+                    ysphere_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), r, kTMin, h,
+                                 motion_frac(S, r.t, ld(&S.runs[ri].movers)));
+                    continue;
+                }
+                ray lr = r;
+                if (ei >= 0) {
+                    const entry_v e = view_entry<true>(S.entries, S.entry_movers, ei);
+                    lr = entry_local_ray<true>(e, r);
+                    if ((F & F_GBVH) && e.bvh_root >= 0) {
+                        group_bvh(S, e.bvh_root, lr, kTMin, h, stk, 0, e.movers);
+                        continue;
+                    }
+                }
+                group_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), lr, kTMin, h, ld(&S.runs[ri].movers));
+            }
         }
         if (F & F_MEDIA) {
             for (int k = 0; k < S.n_media; ++k) {
                 const int ei = ld(&S.media[k]);
-                const entry_v e = view_entry<true>(S.entries, ei);
+                const entry_v e = view_entry<true>(S.entries, S.entry_movers, ei);
                 double t;
                 if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk)) {
                     h.t = t;
@@ -553,11 +681,11 @@ RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d
         return;
     }
     const rtw_prim q = S.prims[h.prim];
-    const entry_v e = view_entry<false>(S.entries, q.entry);
+    const entry_v e = view_entry<false>(S.entries, S.entry_movers, q.entry);
     const ray lr = entry_local_ray<false>(e, r);
     p = at(lr, h.t);
     if (is_sphere(q.type)) {
-        const d3 cc = sphere_center(q, lr.t);
+        const d3 cc = sphere_center(q, lr.t, motion_frac(S, lr.t, q.type >= DP_MOVING_COMMON));
         n = (p - cc) / q.p[3];
     } else {
         n = rect_normal(q.type);
@@ -642,9 +770,9 @@ RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
         const rtw_prim& q = S.prims[L.prim];
         const ray r{o, v, kFltMax};
         double t;
-        if (!sphere_t(q, r, 0.001, __builtin_inf(), t)) return 0.0;
-        const double radius = q.p[3];
-        const double cos_theta_max = __builtin_sqrt(1 - radius * radius / len2(ld3(q.p) - o));
+        if (!sphere_t(q, r, 0.001, __builtin_inf(), t, motion_frac(S, r.t, q.type >= DP_MOVING_COMMON)))
+            return 0.0;
+        const double cos_theta_max = __builtin_sqrt(1 - q.p[9] / len2(ld3(q.p) - o));  // p[9] = radius * radius
         const double solid_angle = kTwoPi * (1.0 - cos_theta_max);
         return 1.0 / solid_angle;
     }
@@ -681,7 +809,7 @@ RTW_D d3 mixture_generate(const scene& S, const onb& uvw, d3 o, uint32_t& rng) {
         const d3 direction = ld3(q.p) - o;
         const double distance_squared = len2(direction);
         basis = onb_from_w(direction);
-        a1 = 1 - q.p[3] * q.p[3] / distance_squared;
+        a1 = 1 - q.p[9] / distance_squared;  // radius * radius / distance_squared
     }
     const double s1 = __builtin_sqrt(a1);
     const double z = sph ? 1 + r2 * (s1 - 1) : s1;

@@ -24,6 +24,7 @@
 // pool order never changes a result, only its speed.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -1187,11 +1188,68 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         mat_aux[2 * k] = 1.0 / ri;
         mat_aux[2 * k + 1] = r0;
     }
+    // Device copy of the prims: sphere records rewritten as rtw_device.h
+    // (DP_MOVING_COMMON) describes -- radius^2, center1 - center0, time1 -
+    // time0 precomputed with the reference's expressions -- and the moving
+    // spheres sharing the first mover's interval tagged so traversal computes
+    // their time fraction once per ray.
+    std::vector<rtw_prim> dprims(d->prims, d->prims + d->n_prims);
+    bool mv_common = false;
+    double mv_t0 = 0.0, mv_den = 1.0;
+    for (rtw_prim& q : dprims) {
+        if (!is_sphere(q.type)) continue;
+        q.p[9] = q.p[3] * q.p[3];
+        if (q.type != RTW_PRIM_MOVING_SPHERE) continue;
+        for (int k = 0; k < 3; ++k) q.p[4 + k] = q.p[4 + k] - q.p[k];
+        q.p[8] = q.p[8] - q.p[7];
+        // the shared fraction must stay finite: (time - t0) is at most ~2^129
+        // in magnitude (light pdf rays carry time FLT_MAX)
+        const bool finite_frac = std::isfinite(q.p[7]) && std::isfinite(q.p[8]) && std::fabs(q.p[8]) >= 1e-200;
+        if (!finite_frac) continue;
+        if (!mv_common) {
+            mv_common = true;
+            mv_t0 = q.p[7];
+            mv_den = q.p[8];
+        }
+        if (std::memcmp(&q.p[7], &mv_t0, 8) != 0 || std::memcmp(&q.p[8], &mv_den, 8) != 0) continue;
+        // y-only mover: x and z stay center0's exactly when dc is +-0 and
+        // center0's component is nonzero (x + +-0 == x for x != 0)
+        const bool y_only = q.p[4] == 0.0 && q.p[6] == 0.0 && q.p[0] != 0.0 && q.p[2] != 0.0;
+        q.type = y_only ? DP_MOVING_COMMON_Y : DP_MOVING_COMMON;
+    }
+    // World list runs: consecutive plain entries (one untransformed group,
+    // no BVH) scan their contiguous prims as one run.
+    std::vector<world_run> runs;
+    std::vector<int32_t> entry_movers(std::max(d->n_entries, 1), 0);
+    for (int e = 0; e < d->n_entries; ++e) {
+        const rtw_entry& E = d->entries[e];
+        for (int i = E.first_prim; i < E.first_prim + E.n_prims; ++i)
+            entry_movers[e] |= dprims[i].type >= DP_MOVING_COMMON ? 1 : 0;
+        const bool plain = E.kind == RTW_ENTRY_GROUP && E.n_ops == 0 && E.bvh_root < 0;
+        if (plain && !runs.empty() && runs.back().entry < 0 &&
+            runs.back().first_prim + runs.back().n_prims == E.first_prim) {
+            runs.back().n_prims += E.n_prims;
+            runs.back().movers |= entry_movers[e];
+            continue;
+        }
+        runs.push_back(world_run{plain ? WORLD_RUN_PLAIN : e, E.first_prim, E.n_prims, entry_movers[e]});
+    }
+    // plain runs of y-only spheres -> ysphere_scan (static ones get dy = 0)
+    for (world_run& R : runs) {
+        if (R.entry != WORLD_RUN_PLAIN || R.n_prims < 2) continue;
+        bool all = true;
+        for (int i = R.first_prim; i < R.first_prim + R.n_prims && all; ++i)
+            all = dprims[i].type == DP_MOVING_COMMON_Y || (dprims[i].type == RTW_PRIM_SPHERE && dprims[i].p[1] != 0.0);
+        if (!all) continue;
+        R.entry = WORLD_RUN_YSPHERES;
+        for (int i = R.first_prim; i < R.first_prim + R.n_prims; ++i)
+            if (dprims[i].type == RTW_PRIM_SPHERE) dprims[i].p[5] = 0.0;
+    }
     std::vector<part> parts = {
         // parts 0..9 are what shading reads; they come first so a small
         // scene's shading data is one contiguous prefix the shade kernel can
         // stage in LDS
-        {d->prims, sizeof(rtw_prim) * d->n_prims, 0},
+        {dprims.data(), sizeof(rtw_prim) * dprims.size(), 0},
         {d->entries, sizeof(rtw_entry) * d->n_entries, 0},
         {d->materials, sizeof(rtw_material) * d->n_materials, 0},
         {d->textures, sizeof(rtw_texture) * d->n_textures, 0},
@@ -1203,6 +1261,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {mat_aux.data(), sizeof(double) * mat_aux.size(), 0},
         {d->bvh_nodes, sizeof(rtw_bvh_node) * d->n_bvh_nodes, 0},
         {d->bvh_items, sizeof(int32_t) * d->n_bvh_items, 0},
+        {runs.data(), sizeof(world_run) * runs.size(), 0},
+        {entry_movers.data(), sizeof(int32_t) * entry_movers.size(), 0},
     };
     size_t total = 0;
     for (auto& p : parts) {
@@ -1230,6 +1290,12 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.mat_aux = (const double*)at(9);
     S.nodes = (const rtw_bvh_node*)at(10);
     S.items = (const int32_t*)at(11);
+    S.runs = (const world_run*)at(12);
+    S.entry_movers = (const int32_t*)at(13);
+    S.n_runs = (int32_t)runs.size();
+    S.mv_common = mv_common ? 1 : 0;
+    S.mv_t0 = mv_t0;
+    S.mv_den = mv_den;
     h->shade_bytes = (uint32_t)parts[10].off;  // the shading prefix
     h->scene_base = base;
     S.n_entries = d->n_entries;
