@@ -596,7 +596,12 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             if (!slab(nd, r.o, inv, widen_lo(kTMin), widen_hi(h.t))) continue;
             if (nd.count > 0) {
                 for (int k = 0; k < nd.count; ++k) {
-                    const entry_v e = view_entry<false>(S.entries, S.entry_movers, S.items[nd.left + k]);
+                    const int it = S.items[nd.left + k];
+                    if (it < 0) {  // plain one-prim entry, its prim stored as ~prim by the upload
+                        arbitrate(S, ~it, r, kTMin, h, fc);
+                        continue;
+                    }
+                    const entry_v e = view_entry<false>(S.entries, S.entry_movers, it);
                     const ray lr = entry_local_ray<false>(e, r);
                     if ((F & F_GBVH) && e.bvh_root >= 0) {
                         group_bvh(S, e.bvh_root, lr, kTMin, h, stk, sp, S.mv_common != 0);

@@ -1245,6 +1245,28 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         for (int i = R.first_prim; i < R.first_prim + R.n_prims; ++i)
             if (dprims[i].type == RTW_PRIM_SPHERE) dprims[i].p[5] = 0.0;
     }
+    // World-BVH leaves reference entries; a plain one-prim entry's item is
+    // replaced by ~prim so the walk tests the prim without reading the entry.
+    std::vector<int32_t> ditems(d->bvh_items, d->bvh_items + d->n_bvh_items);
+    if (d->world_bvh_root >= 0) {
+        std::vector<int> todo{d->world_bvh_root};
+        while (!todo.empty()) {
+            const rtw_bvh_node& N = d->bvh_nodes[todo.back()];
+            todo.pop_back();
+            if (N.count == 0) {
+                todo.push_back(N.left);
+                todo.push_back(N.right);
+                continue;
+            }
+            for (int k = N.left; k < N.left + N.count; ++k) {
+                if (ditems[k] < 0 || ditems[k] >= d->n_entries)
+                    return rtw_fail(RTW_ERR_INVALID, "world bvh item out of range");
+                const rtw_entry& E = d->entries[ditems[k]];
+                if (E.kind == RTW_ENTRY_GROUP && E.n_ops == 0 && E.bvh_root < 0 && E.n_prims == 1)
+                    ditems[k] = ~E.first_prim;
+            }
+        }
+    }
     std::vector<part> parts = {
         // parts 0..9 are what shading reads; they come first so a small
         // scene's shading data is one contiguous prefix the shade kernel can
@@ -1260,7 +1282,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {frames.data(), sizeof(double) * frames.size(), 0},
         {mat_aux.data(), sizeof(double) * mat_aux.size(), 0},
         {d->bvh_nodes, sizeof(rtw_bvh_node) * d->n_bvh_nodes, 0},
-        {d->bvh_items, sizeof(int32_t) * d->n_bvh_items, 0},
+        {ditems.data(), sizeof(int32_t) * ditems.size(), 0},
         {runs.data(), sizeof(world_run) * runs.size(), 0},
         {entry_movers.data(), sizeof(int32_t) * entry_movers.size(), 0},
     };
