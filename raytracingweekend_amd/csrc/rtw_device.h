@@ -514,6 +514,20 @@ struct lds_stack {
     RTW_D int& at(int i) { return p[i * 256]; }
 };
 
+// Inner nodes carry their children's split axis (pad & 3) and whether the
+// left child lies on the upper side of it (pad & 4), set at upload: the
+// child nearer along the ray is pushed last, so it is visited first and the
+// closest hit tightens early.  (Visiting order never changes the result:
+// arbitrate reproduces the list order's tie rule.)
+template <class STK>
+RTW_D void push_children(const rtw_bvh_node& nd, const d3& d, STK& stk, int& sp) {
+    const int ax = nd.pad & 3;
+    const double da = ax == 0 ? d.x : (ax == 1 ? d.y : d.z);
+    const bool left_first = (da >= 0) != ((nd.pad & 4) != 0);
+    stk.at(sp++) = left_first ? nd.right : nd.left;
+    stk.at(sp++) = left_first ? nd.left : nd.right;
+}
+
 RTW_D double widen_lo(double t) { return t > 0 ? t * 0.5 : t * 2.0 - 1e-9; }
 RTW_D double widen_hi(double t) { return t * (1 + 1e-12) + 1e-9; }
 
@@ -531,8 +545,7 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
         if (nd.count > 0) {
             for (int k = 0; k < nd.count; ++k) arbitrate(S, S.items[nd.left + k], r, t_min, h, fc);
         } else if (sp + 2 <= STK::cap) {  // always true: depth checked at upload
-            stk.at(sp++) = nd.right;
-            stk.at(sp++) = nd.left;
+            push_children(nd, r.d, stk, sp);
         }
     }
 }
@@ -610,8 +623,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                     }
                 }
             } else if (sp + 2 <= STK::cap) {  // always true: depth checked at upload
-                stk.at(sp++) = nd.right;
-                stk.at(sp++) = nd.left;
+                push_children(nd, r.d, stk, sp);
             }
         }
         return h;

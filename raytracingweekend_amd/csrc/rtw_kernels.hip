@@ -1267,6 +1267,23 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             }
         }
     }
+    // Inner BVH nodes: the axis along which their children's centres differ
+    // most, and whether the left child is the upper one (push_children).
+    std::vector<rtw_bvh_node> dnodes(d->bvh_nodes, d->bvh_nodes + d->n_bvh_nodes);
+    for (rtw_bvh_node& N : dnodes) {
+        N.pad = 0;
+        if (N.count > 0) continue;
+        const rtw_bvh_node& L = d->bvh_nodes[N.left];
+        const rtw_bvh_node& R = d->bvh_nodes[N.right];
+        int ax = 0;
+        double best = -1.0;
+        for (int k = 0; k < 3; ++k) {
+            const double gap = std::fabs((R.bmin[k] + R.bmax[k]) - (L.bmin[k] + L.bmax[k]));
+            if (gap > best) best = gap, ax = k;
+        }
+        const bool left_upper = (L.bmin[ax] + L.bmax[ax]) > (R.bmin[ax] + R.bmax[ax]);
+        N.pad = ax | (left_upper ? 4 : 0);
+    }
     std::vector<part> parts = {
         // parts 0..9 are what shading reads; they come first so a small
         // scene's shading data is one contiguous prefix the shade kernel can
@@ -1281,7 +1298,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {media.data(), sizeof(int32_t) * media.size(), 0},
         {frames.data(), sizeof(double) * frames.size(), 0},
         {mat_aux.data(), sizeof(double) * mat_aux.size(), 0},
-        {d->bvh_nodes, sizeof(rtw_bvh_node) * d->n_bvh_nodes, 0},
+        {dnodes.data(), sizeof(rtw_bvh_node) * dnodes.size(), 0},
         {ditems.data(), sizeof(int32_t) * ditems.size(), 0},
         {runs.data(), sizeof(world_run) * runs.size(), 0},
         {entry_movers.data(), sizeof(int32_t) * entry_movers.size(), 0},
