@@ -31,7 +31,10 @@ INCLUDES = [f"-I{ROOT / 'include'}", f"-I{CSRC}", f"-I{CSRC / 'host'}", f"-I{CSR
 # emits no FMA), parity needs the same roundings on the device.
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-variable",
           "-Wno-unused-but-set-variable"]
-DEVICE = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+# -fno-slp-vectorize: the SLP vectorizer folds chains of fp64 compares (the
+# rect bounds tests) into i1-vector reductions that gfx950 evaluates lane by
+# lane with cndmask / shift / bitop3 (19 VALU instead of 8 per rect test).
+DEVICE = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
 
 HOST_SOURCES = sorted((CSRC / "host").glob("*.cpp"))
 DEVICE_SOURCES = sorted(CSRC.glob("*.hip"))

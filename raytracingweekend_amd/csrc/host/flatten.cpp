@@ -13,6 +13,7 @@
 // (entry = -1): hittable_pdf only ever queries them through their own
 // pdf_value/random overrides (pdf.h:35-53).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -438,6 +439,15 @@ int rtw_flatten_scene(const scene& sc, int use_bvh, rtw_scene_desc** out) {
 
     int world_root = -1;
     if (use_bvh) {
+        // leaf sizes, measured on 1 MI355X (random_balls world BVH: 1 item
+        // +8 % over 2; Book-2 group BVHs: 2 items, 1 -8 %, 4 -9 %);
+        // RTW_BVH_LEAF_MAX / RTW_BVH_WORLD_LEAF_MAX override them for tuning
+        auto env_leaf = [](const char* name, int dflt) {
+            const char* v = std::getenv(name);
+            return v && *v ? std::max(1, std::min(16, std::atoi(v))) : dflt;
+        };
+        const int leaf_max = env_leaf("RTW_BVH_LEAF_MAX", 2);
+        const int world_leaf_max = env_leaf("RTW_BVH_WORLD_LEAF_MAX", 1);
         // group BVHs over large groups
         for (auto& e : f.entries) {
             if (e.n_prims <= 8) continue;
@@ -448,7 +458,7 @@ int rtw_flatten_scene(const scene& sc, int use_bvh, rtw_scene_desc** out) {
                 it.id = i;
                 its.push_back(it);
             }
-            bvh_builder b{f.nodes, f.items, 2};
+            bvh_builder b{f.nodes, f.items, leaf_max};
             e.bvh_root = b.build(its, 0, (int)its.size());
         }
         // world BVH over entries (media keep list order: see DESIGN.md)
@@ -460,7 +470,7 @@ int rtw_flatten_scene(const scene& sc, int use_bvh, rtw_scene_desc** out) {
                 it.id = i;
                 its.push_back(it);
             }
-            bvh_builder b{f.nodes, f.items, 2};
+            bvh_builder b{f.nodes, f.items, world_leaf_max};
             world_root = b.build(its, 0, (int)its.size());
         }
     }

@@ -6,7 +6,7 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 D=$1; N=$2
 B=$R/raytracingweekend_amd/_build
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -munsafe-fp-atomics -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -munsafe-fp-atomics -fno-slp-vectorize -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
     -I$R/include -I$D -I$D/host -I$D/host/rtw -x hip -c $D/rtw_kernels.hip -o $B/alt_$N.o 2>/dev/null
 host=$(ls $B/*.cpp.o)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $B/alt_$N.o $host -o $B/librtw_$N.so
