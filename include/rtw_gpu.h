@@ -246,7 +246,10 @@ int rtw_scene_upload(int device, const rtw_scene_desc* desc, void** out_handle);
 
 /* Render the samples selected by `params` and ADD, per pixel, the sum of their
  * radiance (summed in increasing sample order, as RayTracingWeekend.cpp:235-239)
- * into accum_rgb[(j*nx + i)*3 + c].  j = 0 is the bottom row. */
+ * into accum_rgb[(j*nx + i)*3 + c].  j = 0 is the bottom row.
+ * RTW_ERR_INVALID when the scene has a BVH and moving spheres and `camera`'s
+ * shutter [time0, time1] is not inside the desc camera's (the BVH boxes of
+ * moving spheres cover that shutter only). */
 int rtw_render_accumulate(void* scene_handle, const rtw_camera_desc* camera,
                           const rtw_render_params* params, double* accum_rgb,
                           rtw_stats* out_stats);

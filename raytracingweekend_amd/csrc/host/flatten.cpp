@@ -156,6 +156,10 @@ struct flattener {
     std::map<const texture*, int> tex_ids;
     bool perlin = false;
     std::string err;
+    // the camera's shutter interval: rays carry times in [shutter0, shutter1]
+    // (camera.h:41), so a moving sphere's BVH box must cover its centres over
+    // that interval -- movement_linear extrapolates outside [time0, time1]
+    double shutter0 = 0.0, shutter1 = 0.0;
 
     int texture_id(const texture* t) {
         auto f = tex_ids.find(t);
@@ -351,15 +355,26 @@ struct flattener {
     }
 
     // --------------------------------------------------------- bounds
-    static void prim_bounds(const rtw_prim& p, double* lo, double* hi) {
+    void prim_bounds(const rtw_prim& p, double* lo, double* hi) const {
         const double* q = p.p;
         switch (p.type) {
         case RTW_PRIM_SPHERE:
         case RTW_PRIM_MOVING_SPHERE: {
             const double r = std::fabs(q[3]);
             for (int a = 0; a < 3; ++a) lo[a] = q[a] - r, hi[a] = q[a] + r;
-            if (p.type == RTW_PRIM_MOVING_SPHERE)
+            if (p.type == RTW_PRIM_MOVING_SPHERE) {
+                // the centre moves along a line: its extremes over the shutter
+                // are the centres at the shutter's ends (sphere.h:22-25), plus
+                // center0 / center1 for good measure
                 for (int a = 0; a < 3; ++a) lo[a] = std::min(lo[a], q[4 + a] - r), hi[a] = std::max(hi[a], q[4 + a] + r);
+                for (double t : {shutter0, shutter1}) {
+                    const double f = (t - q[7]) / (q[8] - q[7]);
+                    for (int a = 0; a < 3; ++a) {
+                        const double c = q[a] + f * (q[4 + a] - q[a]);
+                        lo[a] = std::min(lo[a], c - r), hi[a] = std::max(hi[a], c + r);
+                    }
+                }
+            }
             return;
         }
         case RTW_PRIM_RECT_XY: lo[0] = q[0], hi[0] = q[1], lo[1] = q[2], hi[1] = q[3], lo[2] = hi[2] = q[4]; break;
@@ -421,6 +436,11 @@ int rtw_flatten_scene(const scene& sc, int use_bvh, rtw_scene_desc** out) {
     if (!out) return rtw_fail(RTW_ERR_INVALID, "rtw_flatten_scene: null output");
     *out = nullptr;
     flattener f;
+    {
+        const rtw_camera_desc cd = sc.GetCamera().desc();
+        f.shutter0 = std::min(cd.time0, cd.time1);
+        f.shutter1 = std::max(cd.time0, cd.time1);
+    }
     for (const auto& o : sc.GetWorld().objects) {
         if (!o || !f.add_entry(o.get()))
             return rtw_fail(RTW_ERR_UNSUPPORTED, "rtw_flatten_scene: " + (f.err.empty() ? std::string("null object") : f.err));
@@ -454,7 +474,7 @@ int rtw_flatten_scene(const scene& sc, int use_bvh, rtw_scene_desc** out) {
             std::vector<bvh_item> its;
             for (int i = e.first_prim; i < e.first_prim + e.n_prims; ++i) {
                 bvh_item it;
-                flattener::prim_bounds(f.prims[i], it.lo, it.hi);
+                f.prim_bounds(f.prims[i], it.lo, it.hi);
                 it.id = i;
                 its.push_back(it);
             }

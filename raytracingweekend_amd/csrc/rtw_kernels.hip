@@ -1108,6 +1108,9 @@ struct handle_t {
     int grid = 2048;
     int cus = 256;
     int stack_need = 0;  // deepest BVH stack a traversal of this scene can use
+    // BVH boxes of moving spheres cover the desc camera's shutter only
+    bool bvh_motion = false;
+    double shutter0 = 0.0, shutter1 = 0.0;
     std::vector<hipEvent_t> events;
 };
 
@@ -1379,6 +1382,11 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         if (d->entries[e].bvh_root >= 0) group_depth = std::max(group_depth, depth(d->entries[e].bvh_root));
     const int world_depth = d->world_bvh_root >= 0 ? depth(d->world_bvh_root) : 0;
     h->stack_need = world_depth + group_depth + 2;
+    bool movers = false;
+    for (int k = 0; k < d->n_prims; ++k) movers |= d->prims[k].type == RTW_PRIM_MOVING_SPHERE;
+    h->bvh_motion = movers && d->n_bvh_nodes > 0;
+    h->shutter0 = std::min(d->camera.time0, d->camera.time1);
+    h->shutter1 = std::max(d->camera.time0, d->camera.time1);
     if (h->stack_need > kStack)
         return rtw_fail(RTW_ERR_UNSUPPORTED, "BVH too deep for the traversal stack (" + std::to_string(h->stack_need) +
                                                  " > " + std::to_string(kStack) + " entries)");
@@ -1711,6 +1719,11 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     const uint64_t npix = (uint64_t)n_rows * (uint64_t)R.nx;
     if ((uint64_t)R.nx * R.ny >= (1ull << 32) || npix >= (1ull << 31))
         return rtw_fail(RTW_ERR_INVALID, "image too large for 32-bit pixel ids");
+    if (h->bvh_motion && (std::min(camera->time0, camera->time1) < h->shutter0 ||
+                          std::max(camera->time0, camera->time1) > h->shutter1))
+        return rtw_fail(RTW_ERR_INVALID,
+                        "rtw_render_accumulate: camera shutter outside the one the scene's BVH was built for "
+                        "(moving spheres); flatten the scene with this camera");
     HIPCHK(hipSetDevice(h->device));
     hipStream_t st = h->stream;
 

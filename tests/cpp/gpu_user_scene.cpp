@@ -58,10 +58,57 @@ public:
     }
 };
 
-int main() {
-    const int nx = 64, ny = 48, spp = 8, depth = 50;
-    const uint64_t seed = 9;
-    user_scene us(nx * 1.0 / ny);
+// Every motion class and world-run form the upload derives (rtw_device.h,
+// DP_MOVING_COMMON*, WORLD_RUN_*): a run of y-only movers and static spheres
+// (ysphere_scan), a run broken by a static sphere at y == 0, x-movers, a
+// y-mover at x == 0 (general common mover), movers on a second interval
+// (their own division), a translated group holding a mover, and a moving
+// sphere among the lights (its pdf ray carries time FLT_MAX).
+class motion_scene : public scene {
+public:
+    explicit motion_scene(double aspect) : scene() {
+        auto tex = [](double r, double g, double b) { return std::make_shared<constant_texture>(vec3(r, g, b)); };
+        auto white = std::make_shared<lambertian>(tex(0.73, 0.73, 0.73));
+        auto red = std::make_shared<lambertian>(tex(0.65, 0.05, 0.05));
+        auto light = std::make_shared<diffuse_light>(tex(6.0, 6.0, 6.0));
+        auto glass = std::make_shared<dielectric>(1.5);
+        auto mover = [&](vec3 c0, vec3 c1, double r, std::shared_ptr<material> m, double t0, double t1) {
+            moving_sphere* ms = new moving_sphere(c0, r, m);
+            movement_linear mv;
+            mv.center1 = c1;
+            mv.time0 = t0;
+            mv.time1 = t1;
+            ms->set_movement(mv);
+            return std::shared_ptr<hittable>(ms);
+        };
+        // run 1: y-only movers and static spheres off y == 0 -> ysphere_scan
+        Add(std::make_shared<sphere>(vec3(0.5, -1000, 0.25), 1000, white));
+        for (int k = 0; k < 6; ++k)
+            Add(mover(vec3(-2.5 + k, 0.3, 1.5), vec3(-2.5 + k, 0.3 + 0.1 * k, 1.5), 0.3, k & 1 ? red : white, 0.0, 1.0));
+        Add(std::make_shared<sphere>(vec3(1.7, 0.4, -0.6), 0.4, glass));
+        // a light between the runs
+        auto lamp = std::make_shared<xz_rect>(-1.0, 1.0, -1.0, 1.0, 4.0, light);
+        Add(std::make_shared<flip_normals>(lamp));
+        lights->objects.push_back(lamp);
+        // run 2: a static sphere at y == 0, an x-mover, a y-mover at x == 0,
+        // movers on another interval
+        Add(std::make_shared<sphere>(vec3(-1.8, 0.0, -1.2), 0.35, red));
+        Add(mover(vec3(-0.8, 0.35, -1.4), vec3(-0.5, 0.35, -1.4), 0.35, white, 0.0, 1.0));
+        Add(mover(vec3(0.0, 0.3, -2.0), vec3(0.0, 0.7, -2.0), 0.3, red, 0.0, 1.0));
+        Add(mover(vec3(0.9, 0.3, -2.2), vec3(0.9, 0.9, -2.2), 0.3, white, 0.2, 0.7));
+        Add(mover(vec3(2.0, 0.5, -1.0), vec3(2.3, 0.5, -1.3), 0.3, glass, 0.2, 0.7));
+        // a translated group holding a mover
+        Add(std::make_shared<translate>(mover(vec3(0, 0.25, 0), vec3(0, 0.55, 0), 0.25, red, 0.0, 1.0),
+                                        vec3(-0.6, 0.0, 2.4)));
+        // a moving sphere light (not in the world list)
+        lights->objects.push_back(mover(vec3(2.5, 3.0, 2.0), vec3(2.5, 3.2, 2.0), 0.5, light, 0.0, 1.0));
+        cam = camera(vec3(0.0, 2.0, 7.0), vec3(0.0, 0.5, 0.0), vec3(0.0, 1.0, 0.0), 40.0, aspect, 0.0, 7.0,
+                     0.0, 1.0);
+        background_type = BackgroundType::Gradient;
+    }
+};
+
+static int check_scene(const scene& us, const char* name, int nx, int ny, int spp, int depth, uint64_t seed) {
     int failures = 0;
     for (int bvh = 0; bvh <= 1; ++bvh) {
         rtw_scene_desc* d = nullptr;
@@ -94,11 +141,25 @@ int main() {
         double md = 0;
         for (size_t k = 0; k < cg.size(); ++k) md = std::fmax(md, std::fabs(cg[k] - cr[k]));
         const bool ok = md <= 1e-4 && st.segments == seg && std::isfinite(md);
-        std::printf("bvh=%d max|diff|=%.3e segments gpu=%llu oracle=%llu %s\n", bvh, md,
+        std::printf("%s bvh=%d max|diff|=%.3e segments gpu=%llu oracle=%llu %s\n", name, bvh, md,
                     (unsigned long long)st.segments, (unsigned long long)seg, ok ? "ok" : "MISMATCH");
         failures += !ok;
         rtw_scene_free(h);
         rtw_scene_desc_free(d);
+    }
+    return failures;
+}
+
+int main() {
+    const int nx = 64, ny = 48, spp = 8, depth = 50;
+    int failures = 0;
+    {
+        user_scene us(nx * 1.0 / ny);
+        failures += check_scene(us, "user", nx, ny, spp, depth, 9);
+    }
+    {
+        motion_scene ms(nx * 1.0 / ny);
+        failures += check_scene(ms, "motion", nx, ny, spp, depth, 11);
     }
     std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
     return failures ? 1 : 0;

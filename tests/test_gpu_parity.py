@@ -203,8 +203,10 @@ def test_user_scene_with_every_feature(gpu, tmp_path):
     """A user scene built with the host scene API that exercises what the
     built-in scenes leave out (checker texture, fuzzy metal, hollow glass,
     nested transforms, a flipped light, a default-pdf light, gradient sky,
-    depth of field), flat and with BVHs, GPU vs oracle through the C ABI
-    (tests/cpp/gpu_user_scene.cpp)."""
+    depth of field), and a scene of every motion class / world-run form the
+    upload derives (y-only movers in a branch-free sphere run, x-movers,
+    movers on a second interval, a moving light), flat and with BVHs, GPU vs
+    oracle through the C ABI (tests/cpp/gpu_user_scene.cpp)."""
     import subprocess
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
@@ -219,3 +221,21 @@ def test_user_scene_with_every_feature(gpu, tmp_path):
     assert r.returncode == 0, r.stderr
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "OK (0 failures)" in r.stdout, r.stdout + r.stderr
+
+
+def test_bvh_rejects_a_wider_shutter(gpu):
+    """A scene with moving spheres and a BVH was bounded for its camera's
+    shutter (movement_linear extrapolates outside [time0, time1]); a render
+    with a wider shutter is refused instead of silently culling hits."""
+    import copy
+    from raytracingweekend_amd._abi import RtwError
+    sd = gpu.SceneDesc("random_balls", 1.5, use_bvh=True)
+    ds = gpu.DeviceScene(sd)
+    try:
+        cam = copy.copy(sd.camera)
+        cam.time1 = cam.time1 + 1.0
+        with pytest.raises(RtwError, match="shutter"):
+            ds.render_accumulate(8, 8, 1, 5, camera=cam)
+        ds.render_accumulate(8, 8, 1, 5)  # the scene's own camera renders
+    finally:
+        ds.close()
