@@ -120,10 +120,21 @@ def build_oracle(force: bool = False) -> None:
         _run(["make", "-C", str(ROOT / "oracle"), *targets])
 
 
+def build_test_tools(force: bool = False) -> None:
+    """Test-only HIP programs (tests/cpp/*.hip) -> _build/<name>: checks that
+    run on the card (tests/test_div_hw.py)."""
+    BUILD.mkdir(exist_ok=True)
+    for src in sorted((ROOT / "tests" / "cpp").glob("*.hip")):
+        out = BUILD / src.stem
+        if force or _newer(out, [src, *HEADERS]):
+            _run([HIPCC, *DEVICE, *COMMON, *INCLUDES, "-x", "hip", str(src), "-o", str(out)])
+
+
 def build_all(force: bool = False) -> None:
     build_library(force)
     build_cli(force)
     build_oracle(force)
+    build_test_tools(force)
 
 
 if __name__ == "__main__":

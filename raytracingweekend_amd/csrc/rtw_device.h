@@ -141,6 +141,7 @@ RTW_HD d3 local(const onb& b, d3 a) { return b.u * a.x + b.v * a.y + b.w * a.z; 
 // entries (one untransformed group each) scanned as their contiguous prims;
 // WORLD_RUN_YSPHERES: the same, all spheres for ysphere_scan.
 enum : int { WORLD_RUN_PLAIN = -1, WORLD_RUN_YSPHERES = -2 };
+struct bvh_node32;
 struct world_run {
     int32_t entry, first_prim, n_prims, movers;  // movers: the prims hold DP_MOVING_COMMON*
 };
@@ -150,7 +151,7 @@ struct scene {
     const rtw_material* materials;
     const rtw_texture* textures;
     const rtw_light* lights;
-    const rtw_bvh_node* nodes;
+    const bvh_node32* nodes;  // device BVH nodes (fp32 bounds, rtw_scene_upload)
     const int32_t* items;
     const double* ranvec;
     const int32_t* perm;
@@ -167,6 +168,8 @@ struct scene {
     int32_t n_runs;
     int32_t mv_common;     // some prims are DP_MOVING_COMMON*
     double mv_t0, mv_den;  // their time0 and time1 - time0
+    int32_t fast_div;      // shared-divisor sphere roots allowed in world walks (ysphere_scan)
+    double bvh_bound;      // largest |coordinate| of any device BVH node (make_slab_ray)
 };
 
 // Scene features a traversal kernel is specialised for.
@@ -415,6 +418,41 @@ RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_m
     }
 }
 
+// Shared-divisor quotients (rtw_div.h rcp_hw / div_hw) for the sphere roots
+// of a world walk: every root is (-b -+ sqrt(disc)) / dot(d, d), so a scan
+// over many spheres computes 1 / dot(d, d) once and each root pays one
+// multiply and two fma instead of a full division.  Bit-identical to a / b
+// when the divisor lies in [2^-200, 2^200] and the numerator in
+// [2^-800, 2^100]:
+//  * divisor: checked per walk (false for NaN too);
+//  * numerators: bounded above because the scene is (upload sets
+//    scene::fast_div only when every prim coordinate and radius is within
+//    2^40 and every mover shares the common interval) and the walk's ray is
+//    (|o|, |d| <= 2^40, |fc| <= 2^8, checked here), so |-b -+ sqrt(disc)| < 2^95;
+//  * a numerator below 2^-800 (a grazing root) gives quotients below 2^-599
+//    by either route, rejected alike by t > t_min = 0.001.
+// Lanes that fail the check divide exactly (the branch is skipped when no
+// lane of the wave takes it).  Measured: +3 % random_balls flat (485
+// spheres per walk).  The same sharing for rect tests (1 / d.x, 1 / d.y,
+// 1 / d.z), for scans holding one sphere and for BVH walks cost more in
+// registers than the divisions it saved (Cornell -0.6 ... -2.5 %, random_balls
+// BVH -6 %), so those divide directly.
+RTW_D bool walk_ray_ok(const scene& S, const ray& r, double fc) {
+    constexpr double kB = 0x1p40;
+    return S.fast_div != 0 && __builtin_fabs(r.o.x) <= kB && __builtin_fabs(r.o.y) <= kB &&
+           __builtin_fabs(r.o.z) <= kB && __builtin_fabs(r.d.x) <= kB && __builtin_fabs(r.d.y) <= kB &&
+           __builtin_fabs(r.d.z) <= kB && __builtin_fabs(fc) <= 0x1p8;
+}
+// num / den via the shared reciprocal y, exact a / b on lanes without `ok`
+RTW_D double walk_quot(double num, double den, double y, bool ok) {
+    double q = div_hw(num, den, y);
+    if (__builtin_expect(!ok, 0)) {
+        asm volatile("");  // keeps the exact division behind the branch
+        q = num / den;
+    }
+    return q;
+}
+
 // group_scan for a run of spheres that all move along y only (or not at
 // all): centre (c0.x, c0.y + p[5] * fc, c0.z).  The upload forms such runs
 // (WORLD_RUN_YSPHERES) from DP_MOVING_COMMON_Y spheres and static spheres
@@ -423,6 +461,8 @@ RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_m
 // random_balls list.  Same arithmetic as sphere.h:46-81 per sphere.
 RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, double fc) {
     const double a = dot(r.d, r.d);
+    const bool oka = walk_ray_ok(S, r, fc) && div_hw_ok_b(a);  // world walk: t_min = 0.001
+    const double ya = rcp_hw(a);
     // software-pipelined scalar loads: sphere i+1's record is requested
     // before sphere i is tested, so the scalar-cache latency hides behind
     // the test instead of stalling every iteration
@@ -437,10 +477,10 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
         const double disc = b * b - a * c;
         if (disc > 0) {
             const double sq = __builtin_sqrt(disc);
-            double temp = (-b - sq) / a;
+            double temp = walk_quot(-b - sq, a, ya, oka);
             bool ok = temp < h.t && temp > t_min;
             if (!ok) {
-                temp = (-b + sq) / a;
+                temp = walk_quot(-b + sq, a, ya, oka);
                 ok = temp < h.t && temp > t_min;
             }
             if (ok) {
@@ -474,26 +514,66 @@ RTW_D void arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_sta
     }
 }
 
-// Slab test against padded node bounds over a widened interval: it may keep
-// a node the exact test would drop, never the reverse.
-RTW_D bool slab(const rtw_bvh_node& nd, const d3& o, const d3& inv, double t0, double t1) {
-    double lo = t0, hi = t1;
-    {
-        const double ta = (nd.bmin[0] - o.x) * inv.x, tb = (nd.bmax[0] - o.x) * inv.x;
-        lo = fmax(lo, fmin(ta, tb));
-        hi = fmin(hi, fmax(ta, tb));
+// Device BVH node (rtw_scene_upload): the builder's padded fp64 bounds
+// rounded OUTWARD to fp32, children / leaf range in two ints.  32 B instead
+// of rtw_bvh_node's 64, and the slab test below runs in fp32 (twice the fp64
+// rate on gfx950).
+struct bvh_node32 {
+    float lo[3], hi[3];
+    int32_t a;  // inner: left child; leaf: first item
+    int32_t b;  // inner: right child | pad << 28 (push_children); leaf: -count
+};
+RTW_HD int node_count(const bvh_node32& n) { return n.b < 0 ? -n.b : 0; }
+
+// Per-walk fp32 form of the ray for the slab tests: t = x * inv + oi per
+// axis, with oi = -o * inv moved down (oin, near planes) and up (oif, far
+// planes) by eps = 2^-21 (B + |o|) |inv|, B the largest node coordinate
+// (scene::bvh_bound).  eps covers the fp32 rounding of inv (x * inv is off by
+// at most 2^-23.9 B |inv|) and of oi itself, so x * inv + oin <= (x - o) / d
+// <= x * inv + oif in real arithmetic.  An axis whose |inv| or eps exceeds
+// 2^90 (d.K ~ 0, NaN) never culls: inv = 0, oin = -inf, oif = +inf.
+struct slab_ray {
+    float inv[3], oin[3], oif[3];
+};
+RTW_D slab_ray make_slab_ray(const scene& S, const ray& r) {
+    slab_ray s;
+    const double dd[3] = {r.d.x, r.d.y, r.d.z}, oo[3] = {r.o.x, r.o.y, r.o.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double inv = 1.0 / dd[k];
+        const double oi = -oo[k] * inv;
+        const double eps = 0x1p-21 * (S.bvh_bound + __builtin_fabs(oo[k])) * __builtin_fabs(inv);
+        const bool ok = __builtin_fabs(inv) <= 0x1p90 && eps <= 0x1p90;
+        s.inv[k] = ok ? (float)inv : 0.0f;
+        s.oin[k] = ok ? (float)(oi - eps) : -__builtin_inff();
+        s.oif[k] = ok ? (float)(oi + eps) : __builtin_inff();
     }
-    {
-        const double ta = (nd.bmin[1] - o.y) * inv.y, tb = (nd.bmax[1] - o.y) * inv.y;
-        lo = fmax(lo, fmin(ta, tb));
-        hi = fmin(hi, fmax(ta, tb));
+    return s;
+}
+
+// Slab test of a node over [t0, t1] (already widened by the caller): true
+// whenever the real-arithmetic slab test against the builder's padded fp64
+// bounds is (the fp64 test this replaces was itself conservative that way),
+// so it may keep a node that test would drop, never the reverse.  Per axis
+// the near / far planes' t are bracketed by oin / oif (make_slab_ray); the
+// fp32 rounding of each fma and of t0 / t1 (<= 2^-24 relative) is absorbed
+// by moving the final tn down and tf up by 2^-22 relative + 2^-100 absolute
+// (covers denormal flushing).  Node coordinates are finite and within 2^90
+// (upload), so no NaN arises.
+RTW_D bool slab32(const bvh_node32& nd, const slab_ray& s, float t0, float t1) {
+    float tn = t0, tf = t1;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float an = __builtin_fmaf(nd.lo[k], s.inv[k], s.oin[k]);
+        const float bn = __builtin_fmaf(nd.hi[k], s.inv[k], s.oin[k]);
+        const float af = __builtin_fmaf(nd.lo[k], s.inv[k], s.oif[k]);
+        const float bf = __builtin_fmaf(nd.hi[k], s.inv[k], s.oif[k]);
+        tn = __builtin_fmaxf(tn, __builtin_fminf(an, bn));
+        tf = __builtin_fminf(tf, __builtin_fmaxf(af, bf));
     }
-    {
-        const double ta = (nd.bmin[2] - o.z) * inv.z, tb = (nd.bmax[2] - o.z) * inv.z;
-        lo = fmax(lo, fmin(ta, tb));
-        hi = fmin(hi, fmax(ta, tb));
-    }
-    return lo <= hi;
+    const float tn_adj = __builtin_fmaf(__builtin_fabsf(tn), -0x1p-22f, tn) - 0x1p-100f;
+    const float tf_adj = __builtin_fmaf(__builtin_fabsf(tf), 0x1p-22f, tf) + 0x1p-100f;
+    return tn_adj <= tf_adj;
 }
 
 // BVH traversal stacks.  A private array (scratch memory) by default; the
@@ -520,12 +600,13 @@ struct lds_stack {
 // closest hit tightens early.  (Visiting order never changes the result:
 // arbitrate reproduces the list order's tie rule.)
 template <class STK>
-RTW_D void push_children(const rtw_bvh_node& nd, const d3& d, STK& stk, int& sp) {
-    const int ax = nd.pad & 3;
+RTW_D void push_children(const bvh_node32& nd, const d3& d, STK& stk, int& sp) {
+    const int pad = nd.b >> 28, right = nd.b & 0x0fffffff;
+    const int ax = pad & 3;
     const double da = ax == 0 ? d.x : (ax == 1 ? d.y : d.z);
-    const bool left_first = (da >= 0) != ((nd.pad & 4) != 0);
-    stk.at(sp++) = left_first ? nd.right : nd.left;
-    stk.at(sp++) = left_first ? nd.left : nd.right;
+    const bool left_first = (da >= 0) != ((pad & 4) != 0);
+    stk.at(sp++) = left_first ? right : nd.a;
+    stk.at(sp++) = left_first ? nd.a : right;
 }
 
 RTW_D double widen_lo(double t) { return t > 0 ? t * 0.5 : t * 2.0 - 1e-9; }
@@ -536,14 +617,16 @@ template <class STK>
 RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_state& h, STK& stk, int base,
                      bool movers) {
     const double fc = motion_frac(S, r.t, movers);
-    const d3 inv = d3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
+    const slab_ray sr = make_slab_ray(S, r);
+    const float t0 = (float)widen_lo(t_min);
     int sp = base;
     stk.at(sp++) = root;
     while (sp > base) {
-        const rtw_bvh_node nd = S.nodes[stk.at(--sp)];
-        if (!slab(nd, r.o, inv, widen_lo(t_min), widen_hi(h.t))) continue;
-        if (nd.count > 0) {
-            for (int k = 0; k < nd.count; ++k) arbitrate(S, S.items[nd.left + k], r, t_min, h, fc);
+        const bvh_node32 nd = S.nodes[stk.at(--sp)];
+        if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
+        const int cnt = node_count(nd);
+        if (cnt > 0) {
+            for (int k = 0; k < cnt; ++k) arbitrate(S, S.items[nd.a + k], r, t_min, h, fc);
         } else if (sp + 2 <= STK::cap) {  // always true: depth checked at upload
             push_children(nd, r.d, stk, sp);
         }
@@ -601,15 +684,17 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
     hit_state h{kDblMax, -1, false};
     if constexpr ((F & F_WBVH) != 0 && (F & F_MEDIA) == 0) {
         const double fc = motion_frac(S, r.t, S.mv_common != 0);  // transforms keep the ray's time
-        const d3 inv = d3{1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
+        const slab_ray sr = make_slab_ray(S, r);
+        const float t0 = (float)widen_lo(kTMin);
         int sp = 0;
         stk.at(sp++) = S.world_bvh_root;
         while (sp > 0) {
-            const rtw_bvh_node nd = S.nodes[stk.at(--sp)];
-            if (!slab(nd, r.o, inv, widen_lo(kTMin), widen_hi(h.t))) continue;
-            if (nd.count > 0) {
-                for (int k = 0; k < nd.count; ++k) {
-                    const int it = S.items[nd.left + k];
+            const bvh_node32 nd = S.nodes[stk.at(--sp)];
+            if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
+            const int cnt = node_count(nd);
+            if (cnt > 0) {
+                for (int k = 0; k < cnt; ++k) {
+                    const int it = S.items[nd.a + k];
                     if (it < 0) {  // plain one-prim entry, its prim stored as ~prim by the upload
                         arbitrate(S, ~it, r, kTMin, h, fc);
                         continue;

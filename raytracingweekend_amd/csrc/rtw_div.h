@@ -50,4 +50,38 @@ RTW_HD bool div_rcp_ok_a(double a) {
     return a == 0.0 || (m >= 0x1p-500 && m <= 0x1p500);
 }
 
+#if defined(__HIPCC__)
+// Shared-divisor quotients, bit for bit the compiler's own a / b.
+//
+// hipcc expands an fp64 a / b on gfx950 into
+//   ns = div_scale(b), y0 = rcp(ns), two Newton steps y = fma(y, fma(-ns, y, 1), y),
+//   ns' = div_scale(a), q = ns' * y, r = fma(-ns, q, ns'), div_fmas(r, y, q),
+//   div_fixup(., b, a)
+// where div_scale / div_fmas only rescale operands with extreme exponents and
+// div_fixup only repairs zeros, infinities, NaNs and over/underflow.  When
+// |b| is in [2^-200, 2^200] and |a| in [2^-800, 2^100] none of them acts, and
+// the sequence is exactly rcp_hw(b) followed by div_hw(a, b, y): the
+// reciprocal part depends on b alone, so several quotients by one divisor
+// (a ray direction component, a vector length, a pdf) pay the quarter-rate
+// v_rcp_f64 and its refinement once.  tests/cpp/div_hw_check.hip checks the
+// identity on the card; callers keep exact a / b for lanes outside the range.
+__device__ __forceinline__ double rcp_hw(double b) {
+    const double y0 = __builtin_amdgcn_rcp(b);
+    const double y1 = __builtin_fma(y0, __builtin_fma(-b, y0, 1.0), y0);
+    return __builtin_fma(y1, __builtin_fma(-b, y1, 1.0), y1);
+}
+__device__ __forceinline__ double div_hw(double a, double b, double y) {
+    const double q = a * y;
+    return __builtin_fma(__builtin_fma(-b, q, a), y, q);
+}
+__device__ __forceinline__ bool div_hw_ok_b(double b) {
+    const double m = __builtin_fabs(b);
+    return m >= 0x1p-200 && m <= 0x1p200;
+}
+__device__ __forceinline__ bool div_hw_ok_a(double a) {
+    const double m = __builtin_fabs(a);
+    return m >= 0x1p-800 && m <= 0x1p100;
+}
+#endif
+
 }  // namespace rtwd

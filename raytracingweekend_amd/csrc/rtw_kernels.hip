@@ -1287,6 +1287,27 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         const bool left_upper = (L.bmin[ax] + L.bmax[ax]) > (R.bmin[ax] + R.bmax[ax]);
         N.pad = ax | (left_upper ? 4 : 0);
     }
+    // fp32 device nodes (rtw_device.h bvh_node32): bounds rounded outward;
+    // a BVH whose bounds are not finite within 2^90 is not used at all (the
+    // flat list gives the same image)
+    std::vector<bvh_node32> dnodes32(dnodes.size());
+    double bvh_bound = 0.0;
+    bool bvh_ok = dnodes.size() < (1u << 28);
+    for (size_t k = 0; k < dnodes.size(); ++k) {
+        const rtw_bvh_node& N = dnodes[k];
+        bvh_node32& M = dnodes32[k];
+        for (int j = 0; j < 3; ++j) {
+            bvh_ok = bvh_ok && std::isfinite(N.bmin[j]) && std::isfinite(N.bmax[j]) &&
+                     std::fabs(N.bmin[j]) <= 0x1p90 && std::fabs(N.bmax[j]) <= 0x1p90;
+            float lo = (float)N.bmin[j], hi = (float)N.bmax[j];
+            if ((double)lo > N.bmin[j]) lo = std::nextafter(lo, -INFINITY);
+            if ((double)hi < N.bmax[j]) hi = std::nextafter(hi, INFINITY);
+            M.lo[j] = lo, M.hi[j] = hi;
+            bvh_bound = std::max(bvh_bound, std::max(std::fabs((double)lo), std::fabs((double)hi)));
+        }
+        M.a = N.left;
+        M.b = N.count > 0 ? -N.count : (N.right | (N.pad << 28));
+    }
     std::vector<part> parts = {
         // parts 0..9 are what shading reads; they come first so a small
         // scene's shading data is one contiguous prefix the shade kernel can
@@ -1301,7 +1322,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {media.data(), sizeof(int32_t) * media.size(), 0},
         {frames.data(), sizeof(double) * frames.size(), 0},
         {mat_aux.data(), sizeof(double) * mat_aux.size(), 0},
-        {dnodes.data(), sizeof(rtw_bvh_node) * dnodes.size(), 0},
+        {dnodes32.data(), sizeof(bvh_node32) * dnodes32.size(), 0},
         {ditems.data(), sizeof(int32_t) * ditems.size(), 0},
         {runs.data(), sizeof(world_run) * runs.size(), 0},
         {entry_movers.data(), sizeof(int32_t) * entry_movers.size(), 0},
@@ -1330,7 +1351,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.media = (const int32_t*)at(7);
     S.prim_onb = (const double*)at(8);
     S.mat_aux = (const double*)at(9);
-    S.nodes = (const rtw_bvh_node*)at(10);
+    S.nodes = (const bvh_node32*)at(10);
+    S.bvh_bound = bvh_bound;
     S.items = (const int32_t*)at(11);
     S.runs = (const world_run*)at(12);
     S.entry_movers = (const int32_t*)at(13);
@@ -1338,20 +1360,32 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.mv_common = mv_common ? 1 : 0;
     S.mv_t0 = mv_t0;
     S.mv_den = mv_den;
+    // walk_quot (rtw_device.h): every prim coordinate and radius within 2^40,
+    // every mover on the common interval
+    {
+        bool bounded = true;
+        auto in = [&](double v) { return std::isfinite(v) && std::fabs(v) <= 0x1p40; };
+        for (const rtw_prim& q : dprims) {
+            if (q.type == RTW_PRIM_MOVING_SPHERE) bounded = false;
+            const int np = is_sphere(q.type) ? (q.type == RTW_PRIM_SPHERE ? 4 : 7) : 5;
+            for (int k = 0; k < np; ++k) bounded = bounded && in(q.p[k]);
+        }
+        S.fast_div = bounded ? 1 : 0;
+    }
     h->shade_bytes = (uint32_t)parts[10].off;  // the shading prefix
     h->scene_base = base;
     S.n_entries = d->n_entries;
     S.n_lights = d->n_lights;
     S.light_weight = d->n_lights > 0 ? 1.0 / (double)d->n_lights : 0.0;
-    S.world_bvh_root = d->world_bvh_root;
+    S.world_bvh_root = bvh_ok ? d->world_bvh_root : -1;
     S.render_type = d->render_type;
     S.background = d->background;
     S.n_media = (int32_t)media.size();
     S.has_media = media.empty() ? 0 : 1;
     h->media = !media.empty();
-    h->features = (h->media ? F_MEDIA : 0) | (d->world_bvh_root >= 0 ? F_WBVH : 0);
+    h->features = (h->media ? F_MEDIA : 0) | (bvh_ok && d->world_bvh_root >= 0 ? F_WBVH : 0);
     for (int e = 0; e < d->n_entries; ++e)
-        if (d->entries[e].bvh_root >= 0) h->features |= F_GBVH;
+        if (bvh_ok && d->entries[e].bvh_root >= 0) h->features |= F_GBVH;
     int m = 0;
     for (int k = 0; k < d->n_materials; ++k) {
         const int t = d->materials[k].type;
