@@ -3,7 +3,7 @@
 // chains per wave so latency is hidden).  Prints cycles per wave-instruction
 // per SIMD at the measured clock.  A measurement tool, not part of the product.
 //
-//   hipcc --offload-arch=gfx950 -O3 scripts/valu_rates.hip -o /tmp/valu_rates && /tmp/valu_rates
+//   hipcc --offload-arch=gfx950 -O3 scripts/valu_rates.hip -o scripts/valu_rates.bin && scripts/valu_rates.bin
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
