@@ -170,6 +170,11 @@ struct scene {
     double mv_t0, mv_den;  // their time0 and time1 - time0
     int32_t fast_div;      // shared-divisor sphere roots allowed in world walks (ysphere_scan)
     double bvh_bound;      // largest |coordinate| of any device BVH node (make_slab_ray)
+    // ysphere_scan's fp32 prefilter: per prim {cx, cy, cz, dy, r^2, 0, 0, 0}
+    // (r^2 = +inf: never filtered), and the largest |cx|, |cy|, |dy|, |cz|
+    // and r^2 of the filtered spheres
+    const float* ysph;
+    float ysb_cx, ysb_cy, ysb_dy, ysb_cz, ysb_r2;
 };
 
 // Scene features a traversal kernel is specialised for.
@@ -463,30 +468,53 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
     const double a = dot(r.d, r.d);
     const bool oka = walk_ray_ok(S, r, fc) && div_hw_ok_b(a);  // world walk: t_min = 0.001
     const double ya = rcp_hw(a);
-    // software-pipelined scalar loads: sphere i+1's record is requested
-    // before sphere i is tested, so the scalar-cache latency hides behind
-    // the test instead of stalling every iteration
-    const double* p = S.prims[first].p;
-    double cx = ld(p), cy = ld(p + 1), cz = ld(p + 2), dy = ld(p + 5), rr = ld(p + 9);
+    // fp32 prefilter (twice the fp64 rate): disc32 below -E proves the fp64
+    // disc <= 0 for that lane (no root, nothing to test), so a sphere no lane
+    // of the wave can reach skips the fp64 test altogether.  Each fp32 op is
+    // off by at most u = 2^-24 relative; carried through oc, b, q, c = q - r^2
+    // and disc = b^2 - a c (with b^2 <= a Q, Cauchy-Schwarz) that gives
+    // |disc32 - disc64| <= u a (37 Q + 9 r^2), Q = sum_i (|o_i| + |c_i|)^2;
+    // E = 2^-16 a (Q + r^2) bounds it with |c_i| and r^2 at their scene
+    // maxima over the filtered spheres (host, rounded up) -- about 14 times
+    // over.  NaN anywhere makes the filter pass the sphere on (!(x <= -E)).
+    const float oxf = (float)r.o.x, oyf = (float)r.o.y, ozf = (float)r.o.z;
+    const float dxf = (float)r.d.x, dyf = (float)r.d.y, dzf = (float)r.d.z, fcf = (float)fc;
+    const float af = __builtin_fmaf(dxf, dxf, __builtin_fmaf(dyf, dyf, dzf * dzf));
+    const float R0 = __builtin_fabsf(oxf) + S.ysb_cx;
+    const float R1 = __builtin_fabsf(oyf) + __builtin_fmaf(S.ysb_dy, __builtin_fabsf(fcf), S.ysb_cy);
+    const float R2 = __builtin_fabsf(ozf) + S.ysb_cz;
+    const float E = 0x1p-16f * af * (R0 * R0 + R1 * R1 + R2 * R2 + S.ysb_r2) + 0x1p-60f;  // + denormal slack
+    // software-pipelined scalar loads of the fp32 records: sphere i+1's is
+    // requested before sphere i is filtered
+    const float* f = S.ysph + 8 * (size_t)first;
+    float cx = ld(f), cy = ld(f + 1), cz = ld(f + 2), dy = ld(f + 3), rr = ld(f + 4);
     for (int i = 0; i < n; ++i) {
-        const double* pn = S.prims[first + (i + 1 < n ? i + 1 : i)].p;
-        const double nx = ld(pn), ny = ld(pn + 1), nz = ld(pn + 2), ndy = ld(pn + 5), nrr = ld(pn + 9);
-        const d3 oc{r.o.x - cx, r.o.y - (cy + dy * fc), r.o.z - cz};
-        const double b = dot(oc, r.d);
-        const double c = dot(oc, oc) - rr;
-        const double disc = b * b - a * c;
-        if (disc > 0) {
-            const double sq = __builtin_sqrt(disc);
-            double temp = walk_quot(-b - sq, a, ya, oka);
-            bool ok = temp < h.t && temp > t_min;
-            if (!ok) {
-                temp = walk_quot(-b + sq, a, ya, oka);
-                ok = temp < h.t && temp > t_min;
-            }
-            if (ok) {
-                h.t = temp;
-                h.prim = first + i;
-                h.rect = false;
+        const float* fn = S.ysph + 8 * (size_t)(first + (i + 1 < n ? i + 1 : i));
+        const float nx = ld(fn), ny = ld(fn + 1), nz = ld(fn + 2), ndy = ld(fn + 3), nrr = ld(fn + 4);
+        const float ocx = oxf - cx, ocy = oyf - __builtin_fmaf(dy, fcf, cy), ocz = ozf - cz;
+        const float b32 = __builtin_fmaf(ocx, dxf, __builtin_fmaf(ocy, dyf, ocz * dzf));
+        const float q32 = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
+        const float d32 = __builtin_fmaf(b32, b32, -(af * (q32 - rr)));
+        if (__builtin_amdgcn_ballot_w64(!(d32 <= -E))) {
+            // the reference's test, sphere.h:46-81 (exact fp64)
+            const double* p = S.prims[first + i].p;
+            const d3 oc{r.o.x - ld(p), r.o.y - (ld(p + 1) + ld(p + 5) * fc), r.o.z - ld(p + 2)};
+            const double b = dot(oc, r.d);
+            const double c = dot(oc, oc) - ld(p + 9);
+            const double disc = b * b - a * c;
+            if (disc > 0) {
+                const double sq = __builtin_sqrt(disc);
+                double temp = walk_quot(-b - sq, a, ya, oka);
+                bool ok = temp < h.t && temp > t_min;
+                if (!ok) {
+                    temp = walk_quot(-b + sq, a, ya, oka);
+                    ok = temp < h.t && temp > t_min;
+                }
+                if (ok) {
+                    h.t = temp;
+                    h.prim = first + i;
+                    h.rect = false;
+                }
             }
         }
         cx = nx, cy = ny, cz = nz, dy = ndy, rr = nrr;

@@ -1248,6 +1248,39 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         for (int i = R.first_prim; i < R.first_prim + R.n_prims; ++i)
             if (dprims[i].type == RTW_PRIM_SPHERE) dprims[i].p[5] = 0.0;
     }
+    // ysphere_scan's fp32 prefilter records (rtw_device.h): spheres of
+    // y-sphere runs whose centre (incl. motion) is within 2^8 and radius
+    // within 2^4 are filtered, others (the random_balls ground, r = 1000)
+    // carry r^2 = +inf and always take the fp64 test; the maxima over the
+    // filtered ones bound the prefilter's rounding error
+    std::vector<float> ysph(8 * std::max<size_t>(dprims.size(), 1), 0.0f);
+    float ysb[5] = {0, 0, 0, 0, 0};  // |cx|, |cy|, |dy|, |cz|, r^2 maxima
+    auto up = [](double v) {  // fp32 value >= v
+        float f = (float)v;
+        if ((double)f < v) f = std::nextafter(f, INFINITY);
+        return f;
+    };
+    for (const world_run& R : runs) {
+        if (R.entry != WORLD_RUN_YSPHERES) continue;
+        for (int i = R.first_prim; i < R.first_prim + R.n_prims; ++i) {
+            const rtw_prim& q = dprims[i];
+            float* f = ysph.data() + 8 * (size_t)i;
+            const double dy = q.type == DP_MOVING_COMMON_Y ? q.p[5] : 0.0;
+            f[0] = (float)q.p[0], f[1] = (float)q.p[1], f[2] = (float)q.p[2], f[3] = (float)dy;
+            const bool small = std::fabs(q.p[0]) <= 256 && std::fabs(q.p[1]) <= 256 && std::fabs(dy) <= 256 &&
+                               std::fabs(q.p[2]) <= 256 && std::fabs(q.p[3]) <= 16;
+            if (!small) {
+                f[4] = INFINITY;
+                continue;
+            }
+            f[4] = (float)q.p[9];
+            ysb[0] = std::max(ysb[0], up(std::fabs(q.p[0])));
+            ysb[1] = std::max(ysb[1], up(std::fabs(q.p[1])));
+            ysb[2] = std::max(ysb[2], up(std::fabs(dy)));
+            ysb[3] = std::max(ysb[3], up(std::fabs(q.p[2])));
+            ysb[4] = std::max(ysb[4], up(q.p[9]));
+        }
+    }
     // World-BVH leaves reference entries; a plain one-prim entry's item is
     // replaced by ~prim so the walk tests the prim without reading the entry.
     std::vector<int32_t> ditems(d->bvh_items, d->bvh_items + d->n_bvh_items);
@@ -1326,6 +1359,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {ditems.data(), sizeof(int32_t) * ditems.size(), 0},
         {runs.data(), sizeof(world_run) * runs.size(), 0},
         {entry_movers.data(), sizeof(int32_t) * entry_movers.size(), 0},
+        {ysph.data(), sizeof(float) * ysph.size(), 0},
     };
     size_t total = 0;
     for (auto& p : parts) {
@@ -1356,6 +1390,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.items = (const int32_t*)at(11);
     S.runs = (const world_run*)at(12);
     S.entry_movers = (const int32_t*)at(13);
+    S.ysph = (const float*)at(14);
+    S.ysb_cx = ysb[0], S.ysb_cy = ysb[1], S.ysb_dy = ysb[2], S.ysb_cz = ysb[3], S.ysb_r2 = ysb[4];
     S.n_runs = (int32_t)runs.size();
     S.mv_common = mv_common ? 1 : 0;
     S.mv_t0 = mv_t0;
