@@ -542,6 +542,37 @@ RTW_D void arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_sta
     }
 }
 
+// arbitrate for a world walk's one-prim leaves with the walk's shared
+// 1 / dot(d, d) (walk_quot's rules; t_min = 0.001)
+RTW_D void arbitrate_a(const scene& S, int pi, const ray& r, double t_min, hit_state& h, double fc, double ya,
+                       bool oka) {
+    const rtw_prim q = S.prims[pi];
+    const bool rl = !is_sphere(q.type);
+    double t;
+    if (rl) {
+        if (!rect_t(q, r, t_min, h.t, t)) return;
+    } else {
+        const d3 oc = r.o - sphere_center(q, r.t, fc);
+        const double a = dot(r.d, r.d);
+        const double b = dot(oc, r.d);
+        const double c = dot(oc, oc) - q.p[9];
+        const double disc = b * b - a * c;
+        if (!(disc > 0)) return;
+        const double sq = __builtin_sqrt(disc);
+        t = walk_quot(-b - sq, a, ya, oka);
+        if (!(t < kDblMax && t > t_min)) {
+            t = walk_quot(-b + sq, a, ya, oka);
+            if (!(t < kDblMax && t > t_min)) return;
+        }
+        if (t > h.t) return;
+    }
+    if (better(t, pi, rl, h.t, h.prim, h.rect, h.prim != -1)) {
+        h.t = t;
+        h.prim = pi;
+        h.rect = rl;
+    }
+}
+
 // Device BVH node (rtw_scene_upload): the builder's padded fp64 bounds
 // rounded OUTWARD to fp32, children / leaf range in two ints.  32 B instead
 // of rtw_bvh_node's 64, and the slab test below runs in fp32 (twice the fp64
@@ -737,11 +768,20 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
         int sp = 0;
         stk.at(sp++) = S.world_bvh_root;
         // Leaf items: prims (~prim) or entries (their groups, flat or BVH)
+#ifndef RTW_BVH_SHARE_A
+#define RTW_BVH_SHARE_A 1
+#endif
+        const double a = dot(r.d, r.d);
+        const bool oka = RTW_BVH_SHARE_A && walk_ray_ok(S, r, fc) && div_hw_ok_b(a);
+        const double ya = RTW_BVH_SHARE_A ? rcp_hw(a) : 0.0;
         auto leaf = [&](int la, int lc) {
             for (int k = 0; k < lc; ++k) {
                 const int it = S.items[la + k];
                 if (it < 0) {  // plain one-prim entry, its prim stored as ~prim by the upload
-                    arbitrate(S, ~it, r, kTMin, h, fc);
+                    if (RTW_BVH_SHARE_A)
+                        arbitrate_a(S, ~it, r, kTMin, h, fc, ya, oka);
+                    else
+                        arbitrate(S, ~it, r, kTMin, h, fc);
                     continue;
                 }
                 const entry_v e = view_entry<false>(S.entries, S.entry_movers, it);
