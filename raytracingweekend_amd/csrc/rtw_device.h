@@ -178,7 +178,10 @@ struct scene {
 };
 
 // Scene features a traversal kernel is specialised for.
-enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4 };
+// F_YSPH: the world list holds y-sphere runs (ysphere_scan); without it such
+// runs take group_scan (same results), which keeps the prefilter's code and
+// registers out of the kernels of other scenes (Cornell).
+enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4, F_YSPH = 8 };
 
 // Uniform scene reads.  The scene is read-only for a whole launch; reading
 // it through the constant address space lets the compiler use scalar loads
@@ -850,7 +853,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             for (int ri = 0; ri < S.n_runs; ++ri) {
                 // one scan site for plain runs and transformed groups alike
                 const int ei = ld(&S.runs[ri].entry);
-                if (ei == WORLD_RUN_YSPHERES) {
+                if ((F & F_YSPH) && ei == WORLD_RUN_YSPHERES) {
                     ysphere_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), r, kTMin, h,
                                  motion_frac(S, r.t, ld(&S.runs[ri].movers)));
                     continue;

@@ -1090,6 +1090,7 @@ struct handle_t {
     scene S{};
     bool media = false;
     int features = 0;    // F_MEDIA | F_WBVH | F_GBVH of the uploaded scene
+    bool ysph = false;   // its world list holds y-sphere runs (F_YSPH kernels)
     int shade_mask = 0;  // SF_* material / texture set of the uploaded scene
     const char* scene_base = nullptr;
     uint32_t shade_bytes = 0;  // bytes of the shading prefix of scene_mem
@@ -1420,6 +1421,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.has_media = media.empty() ? 0 : 1;
     h->media = !media.empty();
     h->features = (h->media ? F_MEDIA : 0) | (bvh_ok && d->world_bvh_root >= 0 ? F_WBVH : 0);
+    h->ysph = false;
+    for (const world_run& R : runs) h->ysph = h->ysph || R.entry == WORLD_RUN_YSPHERES;
     for (int e = 0; e < d->n_entries; ++e)
         if (bvh_ok && d->entries[e].bvh_root >= 0) h->features |= F_GBVH;
     int m = 0;
@@ -1553,7 +1556,8 @@ void launch_pk(int cus, size_t shm, hipStream_t st, const scene& S, const job_t&
 }
 
 bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C,
-                    const char* base, uint32_t bytes, int stack_need = kStack) {
+                    const char* base, uint32_t bytes, int stack_need = kStack, bool ysph = false) {
+    if (ysph && !(f & (F_WBVH | F_MEDIA))) f |= F_YSPH;  // world runs are walked: y-sphere scans
     const int pick = pick_shade_mask(mask);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
@@ -1568,6 +1572,7 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     RTW_PER(0, SF_METAL | SF_DIEL, true)
     RTW_PER(0, SF_ALL, true)
     RTW_PER(0, SF_METAL | SF_DIEL, false)
+    RTW_PER(F_YSPH, SF_METAL | SF_DIEL, false)
     RTW_PER(F_WBVH, SF_METAL | SF_DIEL, false)
 #undef RTW_PER
     // general: every material / texture, scene read through the caches, one
@@ -1578,9 +1583,11 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
         return true;                                                  \
     }
     RTW_PER(0)
+    RTW_PER(F_YSPH)
     RTW_PER(F_MEDIA)
     RTW_PER(F_WBVH)
     RTW_PER(F_GBVH)
+    RTW_PER(F_YSPH | F_GBVH)
     RTW_PER(F_MEDIA | F_GBVH)
     RTW_PER(F_WBVH | F_GBVH)
 #undef RTW_PER
@@ -1867,7 +1874,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     const char* mode_env = std::getenv("RTW_MODE");
     const bool persistent = !(mode_env && std::string(mode_env) == "wavefront") &&
                             launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J, C, h->scene_base,
-                                           h->shade_bytes);
+                                           h->shade_bytes, h->stack_need, h->ysph);
 
     for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
@@ -1883,7 +1890,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 HIPCHK(hipEventRecord(h->events[e0], st));
             }
             launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base, h->shade_bytes,
-                           h->stack_need);
+                           h->stack_need, h->ysph);
             HIPCHK(hipGetLastError());
             if (timed) {
                 HIPCHK(hipEventRecord(h->events[e1], st));
