@@ -893,9 +893,12 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
 
 // Reconstruct the hit record (p, normal, material) of a winner exactly as
 // the reference produced it (leaf hit, then ops outward).
+// (MEDIA false: the scene has no isotropic material, hence no medium whose
+// hit this could be.)
+template <bool MEDIA = true>
 RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d3& n, int& mat, bool& rect) {
     rect = false;
-    if (h.prim <= -2) {  // constant_medium, hittable.h:469-472
+    if (MEDIA && h.prim <= -2) {  // constant_medium, hittable.h:469-472
         p = at(r, h.t);
         n = d3{1, 0, 0};
         mat = S.entries[-h.prim - 2].phase_material;

@@ -343,7 +343,7 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
     d3 p, n;
     int mat;
     bool rect;
-    hit_record(S, r, hit_state{t, prim, false}, p, n, mat, rect);
+    hit_record<(M & SF_ISO) != 0>(S, r, hit_state{t, prim, false}, p, n, mat, rect);
     if (S.render_type == RTW_RENDER_NORMAL) {  // :135-136
         E = d3{0.5f, 0.5f, 0.5f} * (n + d3{1, 1, 1});
         return SEG_END;
@@ -809,8 +809,14 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         pk.mark(PS_TRAVERSE);
         // 3. counting sort of the block's paths by key
         uint32_t rank_in_wave = 0;
+        // keys the scene's material set cannot produce are skipped (their
+        // counts stay 0; keep s_kc's slots zero for the prefix below)
+        constexpr auto key_used = [](int k) {
+            return !((k == K_METAL && !(M & SF_METAL)) || (k == K_ISO && !(M & SF_ISO)));
+        };
 #pragma unroll
         for (int k = 0; k < K_N; ++k) {
+            if (!key_used(k)) continue;
             const unsigned long long m = __ballot(key == k);
             if (key == k) rank_in_wave = (uint32_t)__popcll(m & lanemask_lt());
             if (lane == 0) s_kc[wave][k] = (uint32_t)__popcll(m);
@@ -819,6 +825,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         uint32_t dst = rank_in_wave, idle_total = 0;
 #pragma unroll
         for (int k = 0; k < K_N; ++k) {
+            if (!key_used(k)) continue;
             uint32_t tot = 0, before = 0;
 #pragma unroll
             for (int w = 0; w < kSortWaves; ++w) {
