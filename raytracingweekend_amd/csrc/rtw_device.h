@@ -181,7 +181,10 @@ struct scene {
 // F_YSPH: the world list holds y-sphere runs (ysphere_scan); without it such
 // runs take group_scan (same results), which keeps the prefilter's code and
 // registers out of the kernels of other scenes (Cornell).
-enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4, F_YSPH = 8 };
+// F_STATIC: no moving spheres, so a ray's time is never read (sphere.h:22-25
+// is its only reader); the persistent kernels then keep no time per path
+// (the camera still draws it: the RNG sequence is the reference's).
+enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4, F_YSPH = 8, F_STATIC = 16 };
 
 // Uniform scene reads.  The scene is read-only for a whole launch; reading
 // it through the constant address space lets the compiler use scalar loads

@@ -778,6 +778,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
                 if (left) open = false;
                 if (got) {
                     x.r = camera_sample(J, q, x.rng);
+                    if (F & F_STATIC) x.r.t = 0.0;  // never read (F_STATIC)
                     x.q = q;
                     x.depth = (uint32_t)J.max_depth;
                     thr = d3{1.0, 1.0, 1.0};
@@ -842,7 +843,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         // 4. move every path to the slot of its rank
         x_o[0][dst] = x.r.o.x, x_o[1][dst] = x.r.o.y, x_o[2][dst] = x.r.o.z;
         x_d[0][dst] = x.r.d.x, x_d[1][dst] = x.r.d.y, x_d[2][dst] = x.r.d.z;
-        x_tm[dst] = x.r.t;
+        if (!(F & F_STATIC)) x_tm[dst] = x.r.t;
         x_th[0][dst] = thr.x, x_th[1][dst] = thr.y, x_th[2][dst] = thr.z;
         x_t[dst] = th;
         x_prim[dst] = hp;
@@ -851,7 +852,8 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         x_q[dst] = x.q;
         __syncthreads();
         const uint32_t me = threadIdx.x;
-        x.r = ray{d3{x_o[0][me], x_o[1][me], x_o[2][me]}, d3{x_d[0][me], x_d[1][me], x_d[2][me]}, x_tm[me]};
+        x.r = ray{d3{x_o[0][me], x_o[1][me], x_o[2][me]}, d3{x_d[0][me], x_d[1][me], x_d[2][me]},
+                  (F & F_STATIC) ? 0.0 : x_tm[me]};
         thr = d3{x_th[0][me], x_th[1][me], x_th[2][me]};
         th = x_t[me];
         hp = x_prim[me];
@@ -1098,6 +1100,7 @@ struct handle_t {
     bool media = false;
     int features = 0;    // F_MEDIA | F_WBVH | F_GBVH of the uploaded scene
     bool ysph = false;   // its world list holds y-sphere runs (F_YSPH kernels)
+    bool movers = true;  // it holds moving spheres (else F_STATIC kernels)
     int shade_mask = 0;  // SF_* material / texture set of the uploaded scene
     const char* scene_base = nullptr;
     uint32_t shade_bytes = 0;  // bytes of the shading prefix of scene_mem
@@ -1430,6 +1433,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     h->features = (h->media ? F_MEDIA : 0) | (bvh_ok && d->world_bvh_root >= 0 ? F_WBVH : 0);
     h->ysph = false;
     for (const world_run& R : runs) h->ysph = h->ysph || R.entry == WORLD_RUN_YSPHERES;
+    h->movers = false;
+    for (int k = 0; k < d->n_prims; ++k) h->movers = h->movers || d->prims[k].type == RTW_PRIM_MOVING_SPHERE;
     for (int e = 0; e < d->n_entries; ++e)
         if (bvh_ok && d->entries[e].bvh_root >= 0) h->features |= F_GBVH;
     int m = 0;
@@ -1563,18 +1568,21 @@ void launch_pk(int cus, size_t shm, hipStream_t st, const scene& S, const job_t&
 }
 
 bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C,
-                    const char* base, uint32_t bytes, int stack_need = kStack, bool ysph = false) {
+                    const char* base, uint32_t bytes, int stack_need = kStack, bool ysph = false,
+                    bool static_scene = false) {
     if (ysph && !(f & (F_WBVH | F_MEDIA))) f |= F_YSPH;  // world runs are walked: y-sphere scans
     const int pick = pick_shade_mask(mask);
+    const int fs = static_scene ? f | F_STATIC : f;  // specialised kernels only
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
 #define RTW_PER(FF, MM, LL)                                            \
-    if (f == (FF) && pick == (MM) && lds == (LL)) {                  \
+    if ((f == (FF) || fs == (FF)) && pick == (MM) && lds == (LL)) {  \
         if (!probe) launch_pk<FF, MM, LL>(cus, shm, st, S, J, C, base, bytes, stack_need); \
         return true;                                                 \
     }
     // specialised: small list scenes whose shading data fit in LDS, and the
     // lambertian / metal / dielectric sets of the Book-1 scene, flat or BVH
+    RTW_PER(F_STATIC, SF_DIEL, true)
     RTW_PER(0, SF_DIEL, true)
     RTW_PER(0, SF_METAL | SF_DIEL, true)
     RTW_PER(0, SF_ALL, true)
@@ -1881,7 +1889,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     const char* mode_env = std::getenv("RTW_MODE");
     const bool persistent = !(mode_env && std::string(mode_env) == "wavefront") &&
                             launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J, C, h->scene_base,
-                                           h->shade_bytes, h->stack_need, h->ysph);
+                                           h->shade_bytes, h->stack_need, h->ysph, !h->movers);
 
     for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
@@ -1897,7 +1905,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 HIPCHK(hipEventRecord(h->events[e0], st));
             }
             launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base, h->shade_bytes,
-                           h->stack_need, h->ysph);
+                           h->stack_need, h->ysph, !h->movers);
             HIPCHK(hipGetLastError());
             if (timed) {
                 HIPCHK(hipEventRecord(h->events[e1], st));
