@@ -392,15 +392,17 @@ struct hit_state {
 // Linear closest hit over prims [first, first+n) of one group, in list order
 // (t range (t_min, closest]) with the reference's own comparisons; the
 // primitive data are wave-uniform scalar loads.
+// (STATIC: the scene has no moving spheres, centres are center0.)
+template <bool STATIC = false>
 RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, bool movers) {
-    const double fc = motion_frac(S, r.t, movers);
+    const double fc = STATIC ? 0.0 : motion_frac(S, r.t, movers);
     const double a = dot(r.d, r.d);  // sphere.h:50, the same for every sphere
     for (int i = 0; i < n; ++i) {
         const rtw_prim q = uprim(S.prims, first + i);
         if (is_sphere(q.type)) {
             // sphere_t inlined so the winner is written where it is found
             // (no per-prim merge of the running best on the common miss path)
-            const d3 oc = r.o - sphere_center(q, r.t, fc);
+            const d3 oc = r.o - (STATIC ? ld3(q.p) : sphere_center(q, r.t, fc));
             const double b = dot(oc, r.d);
             const double c = dot(oc, oc) - q.p[9];
             const double disc = b * b - a * c;
@@ -870,7 +872,8 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                         continue;
                     }
                 }
-                group_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), lr, kTMin, h, ld(&S.runs[ri].movers));
+                group_scan<(F & F_STATIC) != 0>(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), lr, kTMin, h,
+                                                ld(&S.runs[ri].movers));
             }
         }
         if (F & F_MEDIA) {
@@ -898,7 +901,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
 // the reference produced it (leaf hit, then ops outward).
 // (MEDIA false: the scene has no isotropic material, hence no medium whose
 // hit this could be.)
-template <bool MEDIA = true>
+template <bool MEDIA = true, bool STATIC = false>
 RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d3& n, int& mat, bool& rect) {
     rect = false;
     if (MEDIA && h.prim <= -2) {  // constant_medium, hittable.h:469-472
@@ -912,7 +915,7 @@ RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d
     const ray lr = entry_local_ray<false>(e, r);
     p = at(lr, h.t);
     if (is_sphere(q.type)) {
-        const d3 cc = sphere_center(q, lr.t, motion_frac(S, lr.t, q.type >= DP_MOVING_COMMON));
+        const d3 cc = STATIC ? ld3(q.p) : sphere_center(q, lr.t, motion_frac(S, lr.t, q.type >= DP_MOVING_COMMON));
         n = (p - cc) / q.p[3];
     } else {
         n = rect_normal(q.type);

@@ -330,7 +330,7 @@ enum { SEG_CONTINUE = 0, SEG_END = 1, SEG_END_ZERO = 2 };
 // forward: the radiance of a path is thr * (last emitted / background), thr
 // the product of the reference's per-bounce factors attenuation *
 // scattering_pdf / pdf (or attenuation for specular scatter).
-template <int M>
+template <int M, bool STATIC = false>
 __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, int32_t prim, d3& E, d3& f,
                                           prof_t& pf) {
     const ray r = x.r;
@@ -343,7 +343,7 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
     d3 p, n;
     int mat;
     bool rect;
-    hit_record<(M & SF_ISO) != 0>(S, r, hit_state{t, prim, false}, p, n, mat, rect);
+    hit_record<(M & SF_ISO) != 0, STATIC>(S, r, hit_state{t, prim, false}, p, n, mat, rect);
     if (S.render_type == RTW_RENDER_NORMAL) {  // :135-136
         E = d3{0.5f, 0.5f, 0.5f} * (n + d3{1, 1, 1});
         return SEG_END;
@@ -865,7 +865,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         if (x.depth != 0) {
             prof_t pf;
             d3 E, f;
-            const int out = shade_core<M>(SS, x, th, hp, E, f, pf);
+            const int out = shade_core<M, (F & F_STATIC) != 0>(SS, x, th, hp, E, f, pf);
             if (out == SEG_CONTINUE) {
                 thr = thr * f;
             } else {
