@@ -184,7 +184,10 @@ struct scene {
 // F_STATIC: no moving spheres, so a ray's time is never read (sphere.h:22-25
 // is its only reader); the persistent kernels then keep no time per path
 // (the camera still draws it: the RNG sequence is the reference's).
-enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4, F_YSPH = 8, F_STATIC = 16 };
+// F_LIGHTS: the scene has lights, so every lambertian bounce samples the
+// mixture pdf (RayTracingWeekend.cpp:112-132) and the lights-free branch is
+// compiled out.
+enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4, F_YSPH = 8, F_STATIC = 16, F_LIGHTS = 32 };
 
 // Uniform scene reads.  The scene is read-only for a whole launch; reading
 // it through the constant address space lets the compiler use scalar loads

@@ -330,7 +330,7 @@ enum { SEG_CONTINUE = 0, SEG_END = 1, SEG_END_ZERO = 2 };
 // forward: the radiance of a path is thr * (last emitted / background), thr
 // the product of the reference's per-bounce factors attenuation *
 // scattering_pdf / pdf (or attenuation for specular scatter).
-template <int M, bool STATIC = false>
+template <int M, bool STATIC = false, bool LIGHTS = false>
 __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, int32_t prim, d3& E, d3& f,
                                           prof_t& pf) {
     const ray r = x.r;
@@ -393,7 +393,7 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
         }
         pf.mark(PS_HIT);
         double pdf_val;
-        if (S.n_lights > 0) {  // mixture_pdf(cosine_pdf, hittable_pdf(lights)) pdf.h:55-79
+        if (LIGHTS || S.n_lights > 0) {  // mixture_pdf(cosine_pdf, hittable_pdf(lights)) pdf.h:55-79
             dir = mixture_generate(S, uvw, p, rng);
             pf.mark(PS_SAMPLE);
             const double cw = dot(normalize(dir), uvw.w);
@@ -865,7 +865,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         if (x.depth != 0) {
             prof_t pf;
             d3 E, f;
-            const int out = shade_core<M, (F & F_STATIC) != 0>(SS, x, th, hp, E, f, pf);
+            const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0>(SS, x, th, hp, E, f, pf);
             if (out == SEG_CONTINUE) {
                 thr = thr * f;
             } else {
@@ -1569,10 +1569,11 @@ void launch_pk(int cus, size_t shm, hipStream_t st, const scene& S, const job_t&
 
 bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C,
                     const char* base, uint32_t bytes, int stack_need = kStack, bool ysph = false,
-                    bool static_scene = false) {
+                    bool static_scene = false, bool lights = false) {
     if (ysph && !(f & (F_WBVH | F_MEDIA))) f |= F_YSPH;  // world runs are walked: y-sphere scans
     const int pick = pick_shade_mask(mask);
-    const int fs = static_scene ? f | F_STATIC : f;  // specialised kernels only
+    // specialised kernels only
+    const int fs = f | (static_scene ? F_STATIC : 0) | (static_scene && lights ? F_LIGHTS : 0);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
 #define RTW_PER(FF, MM, LL)                                            \
@@ -1582,6 +1583,7 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     }
     // specialised: small list scenes whose shading data fit in LDS, and the
     // lambertian / metal / dielectric sets of the Book-1 scene, flat or BVH
+    RTW_PER(F_STATIC | F_LIGHTS, SF_DIEL, true)
     RTW_PER(F_STATIC, SF_DIEL, true)
     RTW_PER(0, SF_DIEL, true)
     RTW_PER(0, SF_METAL | SF_DIEL, true)
@@ -1889,7 +1891,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     const char* mode_env = std::getenv("RTW_MODE");
     const bool persistent = !(mode_env && std::string(mode_env) == "wavefront") &&
                             launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J, C, h->scene_base,
-                                           h->shade_bytes, h->stack_need, h->ysph, !h->movers);
+                                           h->shade_bytes, h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0);
 
     for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
@@ -1905,7 +1907,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 HIPCHK(hipEventRecord(h->events[e0], st));
             }
             launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base, h->shade_bytes,
-                           h->stack_need, h->ysph, !h->movers);
+                           h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0);
             HIPCHK(hipGetLastError());
             if (timed) {
                 HIPCHK(hipEventRecord(h->events[e1], st));
