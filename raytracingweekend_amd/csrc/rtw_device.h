@@ -187,7 +187,9 @@ struct scene {
 // F_LIGHTS: the scene has lights, so every lambertian bounce samples the
 // mixture pdf (RayTracingWeekend.cpp:112-132) and the lights-free branch is
 // compiled out.
-enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4, F_YSPH = 8, F_STATIC = 16, F_LIGHTS = 32 };
+// F_BLACK: black background and colour rendering (RayTracingWeekend.cpp:
+// 135-159): a miss emits 0 and the normal-visualisation branch is compiled out.
+enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4, F_YSPH = 8, F_STATIC = 16, F_LIGHTS = 32, F_BLACK = 64 };
 
 // Uniform scene reads.  The scene is read-only for a whole launch; reading
 // it through the constant address space lets the compiler use scalar loads

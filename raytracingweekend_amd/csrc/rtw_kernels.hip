@@ -330,21 +330,21 @@ enum { SEG_CONTINUE = 0, SEG_END = 1, SEG_END_ZERO = 2 };
 // forward: the radiance of a path is thr * (last emitted / background), thr
 // the product of the reference's per-bounce factors attenuation *
 // scattering_pdf / pdf (or attenuation for specular scatter).
-template <int M, bool STATIC = false, bool LIGHTS = false>
+template <int M, bool STATIC = false, bool LIGHTS = false, bool BLACK = false>
 __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, int32_t prim, d3& E, d3& f,
                                           prof_t& pf) {
     const ray r = x.r;
     uint32_t rng = x.rng;
     const uint32_t depth = x.depth;
     if (prim == -1) {
-        E = background(S, r.d);
+        E = BLACK ? d3{0, 0, 0} : background(S, r.d);
         return SEG_END;
     }
     d3 p, n;
     int mat;
     bool rect;
     hit_record<(M & SF_ISO) != 0, STATIC>(S, r, hit_state{t, prim, false}, p, n, mat, rect);
-    if (S.render_type == RTW_RENDER_NORMAL) {  // :135-136
+    if (!BLACK && S.render_type == RTW_RENDER_NORMAL) {  // :135-136
         E = d3{0.5f, 0.5f, 0.5f} * (n + d3{1, 1, 1});
         return SEG_END;
     }
@@ -865,7 +865,8 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         if (x.depth != 0) {
             prof_t pf;
             d3 E, f;
-            const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0>(SS, x, th, hp, E, f, pf);
+            const int out =
+                shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0>(SS, x, th, hp, E, f, pf);
             if (out == SEG_CONTINUE) {
                 thr = thr * f;
             } else {
@@ -1569,11 +1570,12 @@ void launch_pk(int cus, size_t shm, hipStream_t st, const scene& S, const job_t&
 
 bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C,
                     const char* base, uint32_t bytes, int stack_need = kStack, bool ysph = false,
-                    bool static_scene = false, bool lights = false) {
+                    bool static_scene = false, bool lights = false, bool black = false) {
     if (ysph && !(f & (F_WBVH | F_MEDIA))) f |= F_YSPH;  // world runs are walked: y-sphere scans
     const int pick = pick_shade_mask(mask);
     // specialised kernels only
-    const int fs = f | (static_scene ? F_STATIC : 0) | (static_scene && lights ? F_LIGHTS : 0);
+    const int fs = f | (static_scene ? F_STATIC : 0) | (static_scene && lights ? F_LIGHTS : 0) |
+                   (static_scene && lights && black ? F_BLACK : 0);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
 #define RTW_PER(FF, MM, LL)                                            \
@@ -1583,6 +1585,7 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     }
     // specialised: small list scenes whose shading data fit in LDS, and the
     // lambertian / metal / dielectric sets of the Book-1 scene, flat or BVH
+    RTW_PER(F_STATIC | F_LIGHTS | F_BLACK, SF_DIEL, true)
     RTW_PER(F_STATIC | F_LIGHTS, SF_DIEL, true)
     RTW_PER(F_STATIC, SF_DIEL, true)
     RTW_PER(0, SF_DIEL, true)
@@ -1891,7 +1894,8 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     const char* mode_env = std::getenv("RTW_MODE");
     const bool persistent = !(mode_env && std::string(mode_env) == "wavefront") &&
                             launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J, C, h->scene_base,
-                                           h->shade_bytes, h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0);
+                                           h->shade_bytes, h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0,
+                                           h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL);
 
     for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
@@ -1907,7 +1911,8 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 HIPCHK(hipEventRecord(h->events[e0], st));
             }
             launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base, h->shade_bytes,
-                           h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0);
+                           h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0,
+                                           h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL);
             HIPCHK(hipGetLastError());
             if (timed) {
                 HIPCHK(hipEventRecord(h->events[e1], st));
