@@ -575,15 +575,19 @@ struct ray_batch {  // one wave's buffer of generated camera samples (LDS)
 
 // Occupancy: left alone the compiler gives k_persist 160-230 VGPRs (2-3
 // waves per SIMD).  Capping at 128 (4 waves) costs some spilled registers and
-// wins: 2 638 -> 2 980 Msamples/s on Cornell (5 waves spill too much: 2 578).
+// wins: 2 638 -> 2 980 Msamples/s on Cornell (5 waves spilled too much then).
+// The scene-specialised list kernels (F_BLACK: Cornell; F_YSPH with the
+// Book-1 material set: random_balls) are lean enough for 5 waves (96 VGPRs):
+// Cornell +4.5 %, random_balls flat +6.8 %; the BVH and all-feature kernels
+// lose 7-24 % at 5 and keep 4.
 #ifdef RTW_SEG_WAVES
-#define RTW_PERSIST_WAVES(M) RTW_SEG_WAVES
+#define RTW_PERSIST_WAVES(F, M) RTW_SEG_WAVES
 #else
-#define RTW_PERSIST_WAVES(M) 4
+#define RTW_PERSIST_WAVES(F, M) (((F) & F_BLACK) || (((F) & F_YSPH) && (M) != SF_ALL) ? 5 : 4)
 #endif
 // LST: BVH traversal stacks in LDS (one column per lane) instead of scratch.
 template <int F, int M, bool LDS, bool LST = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(M))))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kWaves];
@@ -722,7 +726,7 @@ enum { K_LAMB = 0, K_DIEL, K_METAL, K_ISO, K_EMIT, K_MISS, K_IDLE, K_N };
 constexpr int kSortBlock = RTW_SORT_BLOCK;  // paths regrouped together (one workgroup)
 constexpr int kSortWaves = kSortBlock / 64;
 template <int F, int M, bool LDS>
-__global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(M))))
+__global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_kc[kSortWaves][K_N];  // per wave, lanes per key
