@@ -732,9 +732,15 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
     __shared__ uint32_t s_kc[kSortWaves][K_N];  // per wave, lanes per key
     __shared__ uint32_t s_seg[kSortWaves];
     // the exchange: one path per slot (SoA)
-    __shared__ double x_o[3][kSortBlock], x_d[3][kSortBlock], x_tm[kSortBlock], x_th[3][kSortBlock], x_t[kSortBlock];
+    __shared__ double x_o[3][kSortBlock], x_d[3][kSortBlock], x_tm[kSortBlock], x_t[kSortBlock];
     __shared__ int32_t x_prim[kSortBlock];
-    __shared__ uint32_t x_rng[kSortBlock], x_depth[kSortBlock], x_q[kSortBlock];
+    __shared__ uint32_t x_rng[kSortBlock], x_depth[kSortBlock], x_q[kSortBlock], x_home[kSortBlock];
+    // Path throughputs stay put: each path record (live or idle) owns one
+    // home slot of s_thr and carries its index through the exchange, so the
+    // throughput is read and written only where shading uses it and is never
+    // held in registers across traversal and sort.  A lane whose path ended
+    // keeps the record's slot for the camera sample it takes next.
+    __shared__ double s_thr[3][kSortBlock];
     if (LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(base);
         uint4* dst = reinterpret_cast<uint4*>(s_scene);
@@ -746,7 +752,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
     const int own = blockIdx.x % kQShards;
     path_st x;
     x.depth = 0;
-    d3 thr{1.0, 1.0, 1.0};
+    uint32_t home = threadIdx.x;  // this record's s_thr slot
     bool open = true;  // wave-uniform: the queue may still hold samples
     uint32_t segs = 0;
     prof_t pk;  // section profiler (RTW_PROF builds): refill, traverse, sort, exchange, shade
@@ -785,7 +791,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
                     if (F & F_STATIC) x.r.t = 0.0;  // never read (F_STATIC)
                     x.q = q;
                     x.depth = (uint32_t)J.max_depth;
-                    thr = d3{1.0, 1.0, 1.0};
+                    s_thr[0][home] = 1.0, s_thr[1][home] = 1.0, s_thr[2][home] = 1.0;
                 }
             }
         }
@@ -848,7 +854,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         x_o[0][dst] = x.r.o.x, x_o[1][dst] = x.r.o.y, x_o[2][dst] = x.r.o.z;
         x_d[0][dst] = x.r.d.x, x_d[1][dst] = x.r.d.y, x_d[2][dst] = x.r.d.z;
         if (!(F & F_STATIC)) x_tm[dst] = x.r.t;
-        x_th[0][dst] = thr.x, x_th[1][dst] = thr.y, x_th[2][dst] = thr.z;
+        x_home[dst] = home;
         x_t[dst] = th;
         x_prim[dst] = hp;
         x_rng[dst] = x.rng;
@@ -858,7 +864,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         const uint32_t me = threadIdx.x;
         x.r = ray{d3{x_o[0][me], x_o[1][me], x_o[2][me]}, d3{x_d[0][me], x_d[1][me], x_d[2][me]},
                   (F & F_STATIC) ? 0.0 : x_tm[me]};
-        thr = d3{x_th[0][me], x_th[1][me], x_th[2][me]};
+        home = x_home[me];
         th = x_t[me];
         hp = x_prim[me];
         x.rng = x_rng[me];
@@ -871,8 +877,10 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
             d3 E, f;
             const int out =
                 shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0>(SS, x, th, hp, E, f, pf);
+            const d3 thr{s_thr[0][home], s_thr[1][home], s_thr[2][home]};
             if (out == SEG_CONTINUE) {
-                thr = thr * f;
+                const d3 nt = thr * f;
+                s_thr[0][home] = nt.x, s_thr[1][home] = nt.y, s_thr[2][home] = nt.z;
             } else {
                 const d3 L = out == SEG_END ? thr * E : d3{0, 0, 0};
                 double* o = J.L + 3 * (size_t)x.q;
