@@ -189,7 +189,10 @@ struct scene {
 // compiled out.
 // F_BLACK: black background and colour rendering (RayTracingWeekend.cpp:
 // 135-159): a miss emits 0 and the normal-visualisation branch is compiled out.
-enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4, F_YSPH = 8, F_STATIC = 16, F_LIGHTS = 32, F_BLACK = 64 };
+// F_NOLIGHTS: the scene has no lights, so the mixture-pdf branch of the
+// lambertian bounce is compiled out instead.
+enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4, F_YSPH = 8, F_STATIC = 16, F_LIGHTS = 32, F_BLACK = 64,
+             F_NOLIGHTS = 128 };
 
 // Uniform scene reads.  The scene is read-only for a whole launch; reading
 // it through the constant address space lets the compiler use scalar loads

@@ -330,7 +330,7 @@ enum { SEG_CONTINUE = 0, SEG_END = 1, SEG_END_ZERO = 2 };
 // forward: the radiance of a path is thr * (last emitted / background), thr
 // the product of the reference's per-bounce factors attenuation *
 // scattering_pdf / pdf (or attenuation for specular scatter).
-template <int M, bool STATIC = false, bool LIGHTS = false, bool BLACK = false>
+template <int M, bool STATIC = false, bool LIGHTS = false, bool BLACK = false, bool NOLIGHTS = false>
 __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, int32_t prim, d3& E, d3& f,
                                           prof_t& pf) {
     const ray r = x.r;
@@ -393,7 +393,7 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
         }
         pf.mark(PS_HIT);
         double pdf_val;
-        if (LIGHTS || S.n_lights > 0) {  // mixture_pdf(cosine_pdf, hittable_pdf(lights)) pdf.h:55-79
+        if (LIGHTS || (!NOLIGHTS && S.n_lights > 0)) {  // mixture_pdf(cosine_pdf, hittable_pdf(lights)) pdf.h:55-79
             dir = mixture_generate(S, uvw, p, rng);
             pf.mark(PS_SAMPLE);
             const double cw = dot(normalize(dir), uvw.w);
@@ -684,7 +684,7 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
                                                         : SS.prims[h.prim].material].type);
 #endif
             d3 E, f;
-            const int out = shade_core<M>(SS, x, h.t, h.prim, E, f, pf);
+            const int out = shade_core<M, false, false, false, (F & F_NOLIGHTS) != 0>(SS, x, h.t, h.prim, E, f, pf);
             const d3 thr{s_thr[0][threadIdx.x], s_thr[1][threadIdx.x], s_thr[2][threadIdx.x]};
             if (out == SEG_CONTINUE) {
                 const d3 nt = thr * f;
@@ -875,8 +875,8 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         if (x.depth != 0) {
             prof_t pf;
             d3 E, f;
-            const int out =
-                shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0>(SS, x, th, hp, E, f, pf);
+            const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0,
+                                       (F & F_NOLIGHTS) != 0>(SS, x, th, hp, E, f, pf);
             const d3 thr{s_thr[0][home], s_thr[1][home], s_thr[2][home]};
             if (out == SEG_CONTINUE) {
                 const d3 nt = thr * f;
@@ -1587,7 +1587,7 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     const int pick = pick_shade_mask(mask);
     // specialised kernels only
     const int fs = f | (static_scene ? F_STATIC : 0) | (static_scene && lights ? F_LIGHTS : 0) |
-                   (static_scene && lights && black ? F_BLACK : 0);
+                   (static_scene && lights && black ? F_BLACK : 0) | (lights ? 0 : F_NOLIGHTS);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
 #define RTW_PER(FF, MM, LL)                                            \
@@ -1604,7 +1604,9 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     RTW_PER(0, SF_METAL | SF_DIEL, true)
     RTW_PER(0, SF_ALL, true)
     RTW_PER(0, SF_METAL | SF_DIEL, false)
+    RTW_PER(F_YSPH | F_NOLIGHTS, SF_METAL | SF_DIEL, false)
     RTW_PER(F_YSPH, SF_METAL | SF_DIEL, false)
+    RTW_PER(F_WBVH | F_NOLIGHTS, SF_METAL | SF_DIEL, false)
     RTW_PER(F_WBVH, SF_METAL | SF_DIEL, false)
 #undef RTW_PER
     // general: every material / texture, scene read through the caches, one
