@@ -239,3 +239,22 @@ def test_bvh_rejects_a_wider_shutter(gpu):
         ds.render_accumulate(8, 8, 1, 5)  # the scene's own camera renders
     finally:
         ds.close()
+
+
+@pytest.mark.parametrize("scene,nx,ny,spp", [("random_balls", 320, 200, 4), ("book2_final", 96, 96, 2)])
+def test_bvh_equals_flat_at_size(gpu, scene, nx, ny, spp):
+    """Size-independent check of the traversal shortcuts at sizes the oracle
+    is too slow for: the BVH render (fp32 node bounds and slab tests,
+    while-while walks) and the flat render (random_balls: the y-sphere scan
+    with its fp32 prefilter and shared 1/dot(d, d)) take the same branches on
+    every path, so accumulators and traversal counts are identical."""
+    out = []
+    for bvh in (False, True):
+        ds = gpu.DeviceScene(gpu.SceneDesc(scene, nx / ny, use_bvh=bvh))
+        try:
+            out.append(ds.render_accumulate(nx, ny, spp, 50, seed=5))
+        finally:
+            ds.close()
+    (flat, st_flat), (tree, st_tree) = out
+    assert st_flat["segments"] == st_tree["segments"]
+    assert np.array_equal(flat, tree), f"max diff {np.abs(flat - tree).max()}"
