@@ -1244,15 +1244,23 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         const bool y_only = q.p[4] == 0.0 && q.p[6] == 0.0 && q.p[0] != 0.0 && q.p[2] != 0.0;
         q.type = y_only ? DP_MOVING_COMMON_Y : DP_MOVING_COMMON;
     }
-    // World list runs: consecutive plain entries (one untransformed group,
-    // no BVH) scan their contiguous prims as one run.
+    // World list runs: consecutive plain entries (one group, no BVH, no op
+    // that moves the ray -- flip_normals only turns the normal, which
+    // hit_record applies from the prim's entry) scan their contiguous prims
+    // as one run.  (Cornell: the flipped walls join the plain ones.)
+    auto ray_plain = [](const rtw_entry& E) {
+        if (E.kind != RTW_ENTRY_GROUP || E.bvh_root >= 0) return false;
+        for (int k = 0; k < E.n_ops; ++k)
+            if (E.op[k] != RTW_OP_FLIP) return false;
+        return true;
+    };
     std::vector<world_run> runs;
     std::vector<int32_t> entry_movers(std::max(d->n_entries, 1), 0);
     for (int e = 0; e < d->n_entries; ++e) {
         const rtw_entry& E = d->entries[e];
         for (int i = E.first_prim; i < E.first_prim + E.n_prims; ++i)
             entry_movers[e] |= dprims[i].type >= DP_MOVING_COMMON ? 1 : 0;
-        const bool plain = E.kind == RTW_ENTRY_GROUP && E.n_ops == 0 && E.bvh_root < 0;
+        const bool plain = ray_plain(E);
         if (plain && !runs.empty() && runs.back().entry < 0 &&
             runs.back().first_prim + runs.back().n_prims == E.first_prim) {
             runs.back().n_prims += E.n_prims;
@@ -1322,7 +1330,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
                 if (ditems[k] < 0 || ditems[k] >= d->n_entries)
                     return rtw_fail(RTW_ERR_INVALID, "world bvh item out of range");
                 const rtw_entry& E = d->entries[ditems[k]];
-                if (E.kind == RTW_ENTRY_GROUP && E.n_ops == 0 && E.bvh_root < 0 && E.n_prims == 1)
+                if (ray_plain(E) && E.n_prims == 1)
                     ditems[k] = ~E.first_prim;
             }
         }
