@@ -1,18 +1,32 @@
 """bench.py — Msamples/s of the GPU render loop (the reference's "Trace" span,
-RayTracingWeekend.cpp:211-250) on the north-star workload.
+RayTracingWeekend.cpp:211-250) on the BASELINE.json workloads.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  (N > 1: launched by torch.distributed.run, one process per GPU)
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload T|C4|C2|C3|C5|C1]
+                  [--scaling strong|weak]
 
-One step = one full render of the workload on every rank: rank r renders the
-samples [r*spp, (r+1)*spp) of every pixel (weak scaling: the per-GPU work is
-fixed as N grows), the per-pixel fp64 radiance sums are reduced to rank 0 over
-RCCL, and rank 0 finalises the canvas (sum/spp, gamma 2, clamp).  Inputs (the
-uploaded scene) are resident in HBM before the timed region starts.
+--gpus N > 1 runs one process per GPU: under torch.distributed.run (the
+driver's launch: RANK / WORLD_SIZE / LOCAL_RANK in the environment), or, when
+started directly, bench.py starts torch.distributed.run itself as a child
+process (before anything touches the GPU) and exits with its status.
 
-Prints ONE JSON line on rank 0 with `roofline` (traversal kernel, algorithmic
-68 B per segment over its HIP-event-timed launch durations) and `cpu_baseline`
-(the reference's own code, oracle/_ref/rtw_ref, on the host cores; or the C
+One step = one full render of the workload's image: rank r renders its shard
+of the samples of every pixel (raytracingweekend_amd.distributed.render_step,
+the same step tests/test_distributed.py runs over gloo), the per-pixel fp64
+radiance sums are reduced to rank 0 over RCCL, and rank 0 finalises the canvas
+on the GPU (sum/spp, gamma 2, clamp).  The scene is resident in HBM before the
+timed region; the canvas stays in HBM.
+
+Scaling: "strong" (default) keeps the workload's total samples per pixel and
+splits them over the ranks -- T is 1024 spp whatever N, as the metric reads
+("at fixed W x H x spp x max_depth; 1/2/4/8 GPU"); "weak" renders --spp per
+GPU.  value = all samples of a step / the step's time (max over ranks).
+
+Prints ONE JSON line on rank 0 with `roofline` for the traversal kernel the
+library actually launched (rtw_scene_query names it): HIP-event-timed launch
+durations; the VALU roofline (the binding resource) from the
+PMC record of that kernel, build and workload when one is committed under
+profiles/pmc/, else the §8(d) HBM figure alone; and `cpu_baseline` (the
+reference's own code, oracle/_ref/rtw_ref, on the host cores; or the C
 restatement when that binary is absent).
 """
 from __future__ import annotations
@@ -20,12 +34,11 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
 from pathlib import Path
-
-import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -33,22 +46,25 @@ sys.path.insert(0, str(ROOT))
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"] if (ROOT / "BASELINE.json").exists() else \
     "Msamples/s (rays traced/s) at fixed W×H×spp×max_depth; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# Algorithmic bytes of the roofline kernel come from the library
-# (rtw_stats.bytes_intersect = 68 B per traversal: ray 56 B in, hit 12 B out,
-# SURVEY.md 8(d)).  The default kernel, k_persist, fuses traversal and
-# shading and keeps the path in registers, so these bytes never actually
-# reach HBM: the kernel is fp64-VALU / latency bound.
-
-
-# fp64 VALU issue peak: 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction
+# fp64 VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction
 VALU_PEAK_GINST = 1024 * 2.4 / 4
+PMC_DIR = ROOT / "profiles" / "pmc"
 
-
-def workload_name(args) -> str:
-    name = f"{args.scene} {args.nx}x{args.ny} {args.spp}spp/GPU max_depth {args.depth}" + (" bvh" if args.bvh else "")
-    if (args.scene, args.nx, args.ny, args.spp, args.depth, args.bvh) == ("cornell_box", 800, 800, 1024, 50, False):
-        name += " (north-star target T)"
-    return name
+# BASELINE.json configs; spp is the image's TOTAL samples per pixel
+WORKLOADS = {
+    "T": dict(scene="cornell_box", nx=800, ny=800, spp=1024, depth=50, bvh=False,
+              label="T: Cornell box 800x800x1024spp depth 50 (north-star target)"),
+    "C4": dict(scene="cornell_box", nx=800, ny=800, spp=4096, depth=50, bvh=False,
+               label="C4: Cornell box 800x800x4096spp depth 50"),
+    "C2": dict(scene="random_balls", nx=1200, ny=800, spp=256, depth=50, bvh=False,
+               label="C2: Book-1 random_balls 1200x800x256spp depth 50, flat list"),
+    "C3": dict(scene="random_balls", nx=1200, ny=800, spp=1024, depth=50, bvh=True,
+               label="C3: Book-1 random_balls + BVH 1200x800x1024spp depth 50"),
+    "C5": dict(scene="book2_final", nx=1600, ny=1600, spp=4096, depth=50, bvh=True,
+               label="C5: Book-2 final scene + BVH 1600x1600x4096spp depth 50"),
+    "C1": dict(scene="random_balls", nx=200, ny=100, spp=16, depth=50, bvh=False,
+               label="C1: Book-1 random_balls 200x100x16spp depth 50"),
+}
 
 
 def parse():
@@ -56,19 +72,58 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="cornell_box")
-    ap.add_argument("--nx", type=int, default=800)
-    ap.add_argument("--ny", type=int, default=800)
-    ap.add_argument("--spp", type=int, default=1024, help="samples per pixel per GPU")
-    ap.add_argument("--depth", type=int, default=50)
-    ap.add_argument("--bvh", action="store_true")
+    ap.add_argument("--workload", default="T", choices=sorted(WORKLOADS))
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--scene", default=None, help="override the workload's scene (workload becomes custom)")
+    ap.add_argument("--nx", type=int, default=None)
+    ap.add_argument("--ny", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None,
+                    help="samples per pixel: of the whole image (strong) or per GPU (weak)")
+    ap.add_argument("--depth", type=int, default=None)
+    ap.add_argument("--bvh", action="store_true", default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--paths", type=int, default=0, help="wavefront paths in flight (0 = library default)")
     ap.add_argument("--no-kernel-times", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=0, help="CPU baseline sample: spp of the full image (0 = auto)")
     ap.add_argument("--ppm", default="", help="write the rank-0 canvas of the last step here")
-    return ap.parse_args()
+    a = ap.parse_args()
+    w = dict(WORKLOADS[a.workload])
+    custom = False
+    for k in ("scene", "nx", "ny", "spp", "depth", "bvh"):
+        v = getattr(a, k)
+        if v is not None and v != w[k]:
+            w[k] = v
+            custom = True
+        setattr(a, k, w[k])
+    a.workload_key = "custom" if custom else a.workload
+    a.label = (f"custom: {a.scene} {a.nx}x{a.ny}x{a.spp}spp depth {a.depth}" + (" bvh" if a.bvh else "")) \
+        if custom else w["label"]
+    return a
+
+
+def pmc_key(args) -> str:
+    """What a PMC record must have been taken on: per-segment instruction
+    counts and per-launch bytes depend on the scene, image and depth (spp and
+    GPU count only scale them)."""
+    return f"{args.scene} {args.nx}x{args.ny} depth {args.depth}" + (" bvh" if args.bvh else "")
+
+
+def find_pmc(kernel: str, build: str, key: str, pmc_dir: Path = PMC_DIR):
+    """The committed PMC record for exactly this kernel, build and workload
+    (profiles/pmc/*.json), or None -- a record of another build is never used."""
+    if not pmc_dir.is_dir():
+        return None, "no profiles/pmc directory"
+    seen = []
+    for f in sorted(pmc_dir.glob("*.json")):
+        try:
+            p = json.loads(f.read_text())
+        except ValueError:
+            continue
+        if p.get("kernel") == kernel and p.get("build_id") == build and p.get("workload") == key:
+            return p, f.name
+        seen.append(f"{f.name}: {p.get('kernel')} / {p.get('build_id')} / {p.get('workload')}")
+    return None, "no PMC record for this kernel / build / workload (" + "; ".join(seen) + ")"
 
 
 def cpu_baseline(args, threads: int):
@@ -94,23 +149,70 @@ def cpu_baseline(args, threads: int):
     from raytracingweekend_amd.render import SceneDesc
     sd = SceneDesc(args.scene, args.nx / args.ny, False)
     t0 = time.perf_counter()
-    _, seg = oracle_sums(sd, args.nx, args.ny, spp, args.depth, args.seed, threads=threads)
+    oracle_sums(sd, args.nx, args.ny, spp, args.depth, args.seed, threads=threads)
     dt = time.perf_counter() - t0
     return {"value": round(args.nx * args.ny * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
             "kind": "port", "sample": sample, "seconds": round(dt, 3)}
 
 
+def spawn(args) -> int:
+    """Start torch.distributed.run with one rank per GPU (child process; this
+    process never touches the GPU) and return its exit status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    return subprocess.call(cmd, env={**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+
+
+def roofline(args, kernel, build, seg, ms, launches, algo):
+    """Roofline object of the traversal kernel (per launch averages)."""
+    avg_ms = ms / max(launches, 1)
+    seg_launch = seg / max(launches, 1)
+    hbm_ach = algo / (ms * 1e-3) / 1e9
+    hbm = {"achieved": round(hbm_ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(hbm_ach / HBM_PEAK_GBS, 4), "bytes_per_segment": round(algo / max(seg, 1), 2),
+           "algo_bytes_per_launch": round(algo / max(launches, 1), 1),
+           "definition": "SURVEY.md 8(d): 68 algorithmic bytes per traversal (ray 56 B in, hit 12 B out) x "
+                         "device-counted traversals / HIP-event launch time"}
+    rec, src = find_pmc(kernel, build, pmc_key(args))
+    out = {"kernel": kernel, "build_id": build, "launches": int(launches), "avg_launch_ms": round(avg_ms, 4),
+           "segments_per_launch": round(seg_launch, 1)}
+    if rec is None:
+        out.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm["frac"], "traffic": None, "pmc": src, "hbm": hbm})
+        return out
+    scale = seg_launch / rec["segments_per_launch"]  # PMC bytes per launch, scaled by traversals
+    traffic = round(rec["hbm_bytes_per_launch"] * scale, 1)
+    hbm["traffic"] = traffic
+    ipw = rec["valu_insts_per_wave_segment"]
+    ach = ipw * seg_launch / 64 / (avg_ms * 1e-3) / 1e9
+    out.update({"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
+                "frac": round(ach / VALU_PEAK_GINST, 4), "traffic": traffic,
+                "valu_insts_per_wave_segment": round(ipw, 1), "pmc": src,
+                "definition": "VALU wave-instructions per traversal (SQ_INSTS_VALU of the PMC record of this "
+                              "kernel, build and workload) x device-counted traversals / HIP-event launch time, "
+                              "against 1 wave64 VALU instruction per 4 cycles per SIMD at 2.4 GHz",
+                "hbm": hbm})
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(args))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
     import torch.distributed as dist
     from raytracingweekend_amd import build
+    from raytracingweekend_amd.distributed import gpu_finalize_fn, gpu_render_fn, render_step
     from raytracingweekend_amd.render import DeviceScene, SceneDesc, write_ppm
 
     if not (ROOT / "raytracingweekend_amd" / "librtw.so").exists():
@@ -120,27 +222,19 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    nx, ny, spp, depth = args.nx, args.ny, args.spp, args.depth
-    total_spp = spp * world
+    nx, ny, depth = args.nx, args.ny, args.depth
+    spp_total = args.spp if args.scaling == "strong" else args.spp * world
     sd = SceneDesc(args.scene, nx / ny, args.bvh)
     ds = DeviceScene(sd, local_rank)
+    info = ds.query()
     accum = torch.zeros(nx * ny * 3, dtype=torch.float64, device=dev)
     canvas = torch.zeros_like(accum)
     collect = not args.no_kernel_times
 
     def step(timed: bool):
-        # one render of the workload: radiance sums on every rank, reduced to
-        # rank 0, finalised to the canvas there (RayTracingWeekend.cpp:211-250);
-        # the canvas stays in HBM like the inputs
-        accum.zero_()
-        _, st = ds.render_accumulate(nx, ny, total_spp, depth, args.seed, spp_begin=rank * spp, spp_count=spp,
-                                     accum=accum, collect_kernel_times=collect and timed,
-                                     wavefront_paths=args.paths)
-        if world > 1:
-            dist.reduce(accum, dst=0)
-        if rank == 0:
-            ds.finalize_device(accum, nx, ny, total_spp, canvas)
-        return st, canvas
+        fn = gpu_render_fn(ds, nx, ny, spp_total, depth, args.seed, collect_kernel_times=collect and timed,
+                           wavefront_paths=args.paths)
+        return render_step(fn, gpu_finalize_fn(ds, nx, ny, spp_total), accum, canvas, nx, ny, spp_total)
 
     for _ in range(args.warmup):
         step(False)
@@ -149,81 +243,46 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     stats = []
-    canvas = None
     for _ in range(args.steps):
-        st, canvas = step(True)
-        stats.append(st)
+        st = step(True)
+        if st:
+            stats.append(st)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    samples_per_step = nx * ny * spp * world
     seg = sum(s["segments"] for s in stats)
     ms_isect = sum(s["ms_intersect"] for s in stats)
     launches = sum(s["launches_intersect"] for s in stats)
     algo = sum(s["bytes_intersect"] for s in stats)
-    mode = os.environ.get("RTW_MODE", "persistent")
-    sort_env = os.environ.get("RTW_SORT", "")
-    sorted_pk = sort_env == "1" or (sort_env != "0" and not args.bvh)  # the library's default (launch_pk)
-    kernel = ("k_intersect" if os.environ.get("RTW_SPLIT") == "1" else "k_segment") if mode == "wavefront" \
-        else ("k_persist_sort" if sorted_pk else "k_persist")
+    samples = sum(s["samples"] for s in stats)
     if world > 1:
-        v = torch.tensor([seg, ms_isect, launches, algo], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        v = torch.tensor([seg, ms_isect, launches, algo, samples], dtype=torch.float64, device=dev)
         dist.all_reduce(v)
-        seg_all, ms_all, launches_all, algo_all = float(v[0]), float(v[1]), float(v[2]), float(v[3])
-    else:
-        seg_all, ms_all, launches_all, algo_all = float(seg), ms_isect, float(launches), algo
+        seg, ms_isect, launches, algo, samples = (float(x) for x in v.tolist())
 
     if rank == 0:
+        samples_per_step = nx * ny * spp_total
+        assert int(samples) == samples_per_step * args.steps, "ranks rendered a different number of samples"
         value = samples_per_step * args.steps / elapsed / 1e6
-        roofline = None
-        if collect and ms_all > 0:
-            achieved = algo_all / (ms_all * 1e-3) / 1e9
-            traffic, valu = None, None
-            pmc = ROOT / "profiles" / "pmc_intersect.json"
-            workload = workload_name(args)
-            if pmc.exists():
-                try:
-                    p = json.loads(pmc.read_text())
-                except ValueError:
-                    p = {}
-                # PMC figures only describe the workload (and kernel) they were taken on
-                if p.get("workload") == workload and p.get("kernel") == kernel:
-                    # per launch, scaled from the profiled launches by traversals
-                    scale = (seg_all / max(launches_all, 1)) / p["segments_per_launch"]
-                    traffic = round(p["hbm_bytes_per_launch"] * scale, 1)
-                    ipw = p.get("valu_insts_per_wave_segment")
-                    if ipw:
-                        ach = ipw * seg_all / 64 / (ms_all * 1e-3) / 1e9
-                        valu = {"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST,
-                                "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_GINST, 4),
-                                "insts_per_wave_segment": round(ipw, 1),
-                                "source": "profiles/pmc_intersect.json (SQ_INSTS_VALU)"}
-            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "kernel": kernel, "launches": int(launches_all),
-                        "avg_launch_ms": round(ms_all / max(launches_all, 1), 4),
-                        "algo_bytes_per_launch": round(algo_all / max(launches_all, 1), 1),
-                        "bytes_per_segment": round(algo_all / max(seg_all, 1), 2)}
-            if valu:
-                roofline["valu"] = valu
+        roof = roofline(args, info["kernel"], info["build_id"], seg, ms_isect, launches, algo) \
+            if collect and ms_isect > 0 else None
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic",
-            "config": {"workload": workload_name(args),
-                       "scene": args.scene, "nx": nx, "ny": ny, "spp_per_gpu": spp, "max_depth": depth,
-                       "bvh": args.bvh, "parallelism": f"spp-shard x{world} + RCCL reduce"},
-            "msegments_per_s": round(seg_all / args.steps / (elapsed / args.steps) / 1e6, 2) if seg_all else None,
-            "segments_per_sample": round(seg_all / (samples_per_step * args.steps), 4),
-            "ms_render_gpu": round(sum(s["ms_total"] for s in stats) / len(stats), 3),
-            "roofline": roofline,
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (the reference's own scene definitions, seeded RNG)",
+            "config": {"workload": args.label, "workload_id": args.workload_key, "scene": args.scene, "nx": nx,
+                       "ny": ny, "spp_total": spp_total, "spp_per_gpu": spp_total / world, "max_depth": depth,
+                       "bvh": args.bvh, "global_batch": samples_per_step,
+                       "parallelism": f"spp-shard x{world}" + (" + RCCL reduce" if world > 1 else "")},
+            "msegments_per_s": round(seg / elapsed / 1e6, 2) if seg else None,
+            "segments_per_sample": round(seg / max(samples, 1), 4),
+            "ms_render_gpu": round(sum(s["ms_total"] for s in stats) / max(len(stats), 1), 3),
+            "roofline": roof,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

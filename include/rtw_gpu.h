@@ -267,6 +267,70 @@ int rtw_write_ppm(const char* path, const double* canvas_rgb, int nx, int ny);
 
 void rtw_scene_free(void* scene_handle);
 
+/* ------------------------------------------------------------------ */
+/* multi-GPU: one process, one host thread per device, RCCL reduce     */
+/* ------------------------------------------------------------------ */
+
+/* The render of rtw_render_accumulate on ngpus scene handles at once -- the
+ * reference's triple `_for` (RayTracingWeekend.cpp:211-239) spread over the
+ * GPUs of one node.  handles[g] are scenes uploaded (rtw_scene_upload) from
+ * the same desc to ngpus DISTINCT devices.  The sample range [spp_begin,
+ * spp_begin + spp_count) of `params` is split into ngpus contiguous shards
+ * (shard g on handles[g]; SURVEY.md 8(e) sample sharding: every GPU sees the
+ * same pixel-cost mix); each device sums its shard per pixel into a zeroed
+ * buffer of its own, one grouped RCCL reduce (ncclSum over ncclFloat64)
+ * brings the sums to handles[0]'s device, and the result is ADDED into
+ * accum_root: a host pointer, or (params->accum_on_device) a device pointer
+ * on handles[0]'s device.  Rows (row_begin / row_step) are as in
+ * rtw_render_accumulate, on every device.  The reduce reorders the fp64
+ * additions of a pixel's sample sums (~1e-16 relative); with ngpus = 1 the
+ * result is bit-identical to rtw_render_accumulate.  out_stats: samples,
+ * segments, launches and ms_intersect summed over the devices, ms_total = wall
+ * time of the call.  The RCCL communicator of a device set is created on
+ * first use (ncclCommInitAll) and cached until rtw_release_communicators. */
+int rtw_render_multi(int ngpus, void* const* scene_handles, const rtw_camera_desc* camera,
+                     const rtw_render_params* params, double* accum_root, rtw_stats* out_stats);
+
+/* Destroy the cached RCCL communicators of rtw_render_multi. */
+void rtw_release_communicators(void);
+
+/* ------------------------------------------------------------------ */
+/* introspection                                                       */
+/* ------------------------------------------------------------------ */
+typedef struct rtw_scene_info {
+    int32_t device;
+    int32_t n_world_runs;     /* world list as the list kernels walk it        */
+    int32_t n_ysphere_runs;   /* ... runs scanned by the y-sphere scan         */
+    int32_t n_plain_runs;     /* ... other runs of contiguous plain prims      */
+    int32_t features;         /* traversal feature bits of the render kernel  */
+    int32_t shade_mask;       /* material / texture set bits                  */
+    int32_t shade_lds_bytes;  /* shading data staged in LDS per workgroup     */
+    int32_t bvh_lds_nodes;    /* BVH nodes staged in LDS per workgroup        */
+    char kernel[128];         /* traversal kernel a render of this handle
+                                 launches now, e.g. "k_persist_sort<112, 8, true>"
+                                 (RTW_MODE / RTW_SORT / RTW_SPLIT respected) */
+    char build_id[48];        /* hash of the device code's sources and flags  */
+} rtw_scene_info;
+
+int rtw_scene_query(void* scene_handle, rtw_scene_info* out);
+
+/* Hash of the device code's sources and compile flags (rtw_scene_info). */
+const char* rtw_build_id(void);
+
+/* ------------------------------------------------------------------ */
+/* output on the device                                                */
+/* ------------------------------------------------------------------ */
+
+/* The PPM channel bytes of a device canvas, on the GPU:
+ * out[(j*nx+i)*3+c] = int(255.99f * canvas[(j*nx+i)*3+c]) with x86's int()
+ * (truncation; NaN / out of range -> INT_MIN), RayTracingWeekend.cpp:266-270.
+ * canvas_dev, out_dev: device buffers of the handle's device. */
+int rtw_quantize_canvas_device(void* scene_handle, const double* canvas_dev, int nx, int ny, int32_t* out_dev);
+
+/* P3 PPM from quantized channels (rtw_quantize_canvas_device, copied to the
+ * host): rows ny-1..0, "r g b\n" (RayTracingWeekend.cpp:257-276). */
+int rtw_write_ppm_quantized(const char* path, const int32_t* rgb, int nx, int ny);
+
 /* Thread-local message for the last failing call on this thread. */
 const char* rtw_last_error(void);
 

@@ -91,6 +91,19 @@ class rtw_stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class rtw_scene_info(C.Structure):
+    _fields_ = [("device", C.c_int32), ("n_world_runs", C.c_int32), ("n_ysphere_runs", C.c_int32),
+                ("n_plain_runs", C.c_int32), ("features", C.c_int32), ("shade_mask", C.c_int32),
+                ("shade_lds_bytes", C.c_int32), ("bvh_lds_nodes", C.c_int32), ("kernel", C.c_char * 128),
+                ("build_id", C.c_char * 48)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["kernel"] = d["kernel"].decode()
+        d["build_id"] = d["build_id"].decode()
+        return d
+
+
 # exported symbols and their signatures (the C ABI of include/rtw_gpu.h)
 SIGNATURES = {
     "rtw_device_count": (C.c_int, []),
@@ -106,6 +119,13 @@ SIGNATURES = {
     "rtw_scene_builtin": (C.c_int, [C.c_char_p, C.c_double, C.c_int, C.POINTER(C.POINTER(rtw_scene_desc))]),
     "rtw_scene_desc_free": (None, [C.POINTER(rtw_scene_desc)]),
     "rtw_abi_version": (C.c_int, []),
+    "rtw_render_multi": (C.c_int, [C.c_int, C.POINTER(C.c_void_p), C.POINTER(rtw_camera_desc),
+                                   C.POINTER(rtw_render_params), C.c_void_p, C.POINTER(rtw_stats)]),
+    "rtw_release_communicators": (None, []),
+    "rtw_scene_query": (C.c_int, [C.c_void_p, C.POINTER(rtw_scene_info)]),
+    "rtw_build_id": (C.c_char_p, []),
+    "rtw_quantize_canvas_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "rtw_write_ppm_quantized": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
 }
 
 _lib = None

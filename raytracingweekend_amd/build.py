@@ -11,6 +11,7 @@ Run:  python -m raytracingweekend_amd.build [--force]
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -39,6 +40,19 @@ DEVICE = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
 HOST_SOURCES = sorted((CSRC / "host").glob("*.cpp"))
 DEVICE_SOURCES = sorted(CSRC.glob("*.hip"))
 HEADERS = sorted(list(CSRC.rglob("*.h")) + [ROOT / "include" / "rtw_gpu.h"])
+# RCCL for rtw_render_multi (multi.cpp); the same librccl.so.1 torch loads
+LIBS = ["-L/opt/rocm/lib", "-lrccl"]
+
+
+def build_id(extra=()) -> str:
+    """Hash of the device code: kernel sources, headers and compile flags
+    (compiled in as RTW_BUILD_ID; bench.py matches PMC files against it)."""
+    h = hashlib.sha1()
+    for f in [*DEVICE_SOURCES, *HEADERS]:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    h.update(" ".join([*DEVICE, *COMMON, *extra]).encode())
+    return h.hexdigest()[:16]
 
 
 def _newer(target: Path, deps) -> bool:
@@ -59,7 +73,8 @@ def _compile(src: Path, force: bool, extra=(), tag: str = "") -> Path:
     obj = BUILD / (src.name + tag + ".o")
     if force or _newer(obj, [src, *HEADERS, Path(__file__)]):
         if src.suffix == ".hip":
-            cmd = [HIPCC, *DEVICE, *COMMON, *extra, *INCLUDES, "-x", "hip", "-c", str(src), "-o", str(obj)]
+            bid = f'-DRTW_BUILD_ID="{build_id(extra)}"'
+            cmd = [HIPCC, *DEVICE, *COMMON, *extra, bid, *INCLUDES, "-x", "hip", "-c", str(src), "-o", str(obj)]
         else:
             cmd = [HIPCC, *COMMON, *extra, *INCLUDES, "-c", str(src), "-o", str(obj)]
         _run(cmd)
@@ -72,7 +87,7 @@ def build_library(force: bool = False) -> Path:
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
     if force or _newer(LIB, objs):
-        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)])
+        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), *LIBS, "-o", str(LIB)])
     return LIB
 
 
@@ -84,7 +99,7 @@ def build_variant_library(name: str, defines, force: bool = False) -> Path:
     objs = [_compile(s, force, [f"-D{d}" for d in defines], f".{name}") for s in DEVICE_SOURCES]
     objs += [_compile(s, force) for s in HOST_SOURCES]
     if force or _newer(out, objs):
-        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), "-o", str(out)])
+        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), *LIBS, "-o", str(out)])
     return out
 
 
@@ -97,7 +112,7 @@ def build_profiling_library(force: bool = False) -> Path:
     objs = [_compile(s, force, ["-DRTW_PROF"], ".prof") for s in DEVICE_SOURCES]
     objs += [_compile(s, force) for s in HOST_SOURCES]
     if force or _newer(out, objs):
-        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), "-o", str(out)])
+        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), *LIBS, "-o", str(out)])
     return out
 
 

@@ -18,6 +18,7 @@
 #include <map>
 #include <string>
 #include <vector>
+#include "rtw/flatten.h"
 #include "rtw/scene.h"
 #include "rtw_host_util.h"
 
@@ -433,20 +434,30 @@ struct flattener {
 }  // namespace
 
 int rtw_flatten_scene(const scene& sc, int use_bvh, rtw_scene_desc** out) {
+    return rtw_flatten_world(sc.GetWorld(), sc.GetLights().get(), sc.GetCamera(), static_cast<int>(sc.GetRenderType()),
+                             static_cast<int>(sc.GetBackgroundType()), use_bvh, out);
+}
+
+int rtw_flatten_world(const hittable_list& world, const hittable_list* lights, const camera& cam, int render_type,
+                      int background, int use_bvh, rtw_scene_desc** out) {
     if (!out) return rtw_fail(RTW_ERR_INVALID, "rtw_flatten_scene: null output");
     *out = nullptr;
+    if (render_type != RTW_RENDER_SHADED && render_type != RTW_RENDER_NORMAL)
+        return rtw_fail(RTW_ERR_INVALID, "rtw_flatten_scene: unknown render type");
+    if (background != RTW_BG_BLACK && background != RTW_BG_GRADIENT)
+        return rtw_fail(RTW_ERR_INVALID, "rtw_flatten_scene: unknown background type");
     flattener f;
     {
-        const rtw_camera_desc cd = sc.GetCamera().desc();
+        const rtw_camera_desc cd = cam.desc();
         f.shutter0 = std::min(cd.time0, cd.time1);
         f.shutter1 = std::max(cd.time0, cd.time1);
     }
-    for (const auto& o : sc.GetWorld().objects) {
+    for (const auto& o : world.objects) {
         if (!o || !f.add_entry(o.get()))
             return rtw_fail(RTW_ERR_UNSUPPORTED, "rtw_flatten_scene: " + (f.err.empty() ? std::string("null object") : f.err));
     }
-    if (auto L = sc.GetLights()) {
-        for (const auto& o : L->objects)
+    if (lights) {
+        for (const auto& o : lights->objects)
             if (!o || !f.add_light(o.get())) return rtw_fail(RTW_ERR_UNSUPPORTED, "rtw_flatten_scene: light: " + f.err);
     }
     const int n_world = (int)f.prims.size();
@@ -499,8 +510,8 @@ int rtw_flatten_scene(const scene& sc, int use_bvh, rtw_scene_desc** out) {
     rtw_scene_desc* d = new rtw_scene_desc;
     std::memset(d, 0, sizeof *d);
     d->abi_version = RTW_ABI_VERSION;
-    d->render_type = sc.GetRenderType() == RenderType::Normal ? RTW_RENDER_NORMAL : RTW_RENDER_SHADED;
-    d->background = sc.GetBackgroundType() == BackgroundType::Gradient ? RTW_BG_GRADIENT : RTW_BG_BLACK;
+    d->render_type = render_type;
+    d->background = background;
     d->n_prims = (int)f.prims.size();
     d->n_entries = (int)f.entries.size();
     d->n_materials = (int)f.mats.size();
@@ -529,7 +540,7 @@ int rtw_flatten_scene(const scene& sc, int use_bvh, rtw_scene_desc** out) {
         d->perlin_ranvec = rtw_dup(rv);
         d->perlin_perm = rtw_dup(pm);
     }
-    d->camera = sc.GetCamera().desc();
+    d->camera = cam.desc();
     *out = d;
     return RTW_OK;
 }

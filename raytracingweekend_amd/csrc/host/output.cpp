@@ -53,6 +53,22 @@ extern "C" int rtw_write_ppm(const char* path, const double* canvas, int nx, int
     return ok ? RTW_OK : rtw_fail(RTW_ERR_INVALID, "rtw_write_ppm: write failed");
 }
 
+// The same file from channels already quantized on the device
+// (rtw_quantize_canvas_device): rows ny-1..0, "r g b\n".
+extern "C" int rtw_write_ppm_quantized(const char* path, const int32_t* rgb, int nx, int ny) {
+    if (!path || !rgb || nx <= 0 || ny <= 0) return rtw_fail(RTW_ERR_INVALID, "rtw_write_ppm_quantized: bad argument");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return rtw_fail(RTW_ERR_INVALID, std::string("rtw_write_ppm_quantized: cannot open ") + path);
+    std::fprintf(f, "P3\n%d %d\n255\n", nx, ny);
+    for (int j = ny - 1; j >= 0; --j)
+        for (int i = 0; i < nx; ++i) {
+            const int32_t* q = rgb + ((size_t)j * nx + i) * 3;
+            std::fprintf(f, "%d %d %d\n", q[0], q[1], q[2]);
+        }
+    const bool ok = std::fclose(f) == 0;
+    return ok ? RTW_OK : rtw_fail(RTW_ERR_INVALID, "rtw_write_ppm_quantized: write failed");
+}
+
 static inline uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -3,6 +3,7 @@
 // evaluated by the device shade kernel (raytracingweekend_amd/csrc/rtw_device.h).
 #pragma once
 #include <memory>
+#include <random>  // as the reference's material.h:3: scene code draws with std::minstd_rand
 #include "texture.h"
 
 class material {

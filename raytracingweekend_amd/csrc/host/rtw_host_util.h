@@ -17,3 +17,8 @@ T* rtw_dup(const std::vector<T>& v) {
     std::memcpy(p, v.data(), v.size() * sizeof(T));
     return p;
 }
+
+// Internal entry points of the kernel translation unit (rtw_kernels.hip) for
+// the host library (multi.cpp); not part of the C ABI.
+int rtw_handle_device(void* handle);                                             // -1 for null
+int rtw_handle_add_device(void* handle, double* dst, const double* src, size_t n);  // dst += src, synchronous

@@ -1113,6 +1113,7 @@ struct handle_t {
     bool media = false;
     int features = 0;    // F_MEDIA | F_WBVH | F_GBVH of the uploaded scene
     bool ysph = false;   // its world list holds y-sphere runs (F_YSPH kernels)
+    int n_runs = 0, n_ysph_runs = 0, n_plain_runs = 0;  // world-list run layout (rtw_scene_query)
     bool movers = true;  // it holds moving spheres (else F_STATIC kernels)
     int shade_mask = 0;  // SF_* material / texture set of the uploaded scene
     const char* scene_base = nullptr;
@@ -1454,6 +1455,12 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     h->features = (h->media ? F_MEDIA : 0) | (bvh_ok && d->world_bvh_root >= 0 ? F_WBVH : 0);
     h->ysph = false;
     for (const world_run& R : runs) h->ysph = h->ysph || R.entry == WORLD_RUN_YSPHERES;
+    h->n_runs = (int)runs.size();
+    h->n_ysph_runs = h->n_plain_runs = 0;
+    for (const world_run& R : runs) {
+        h->n_ysph_runs += R.entry == WORLD_RUN_YSPHERES;
+        h->n_plain_runs += R.entry == WORLD_RUN_PLAIN;
+    }
     h->movers = false;
     for (int k = 0; k < d->n_prims; ++k) h->movers = h->movers || d->prims[k].type == RTW_PRIM_MOVING_SPHERE;
     for (int e = 0; e < d->n_entries; ++e)
@@ -1511,16 +1518,29 @@ int pick_shade_mask(int mask) {
     return SF_ALL;
 }
 
+// Kernel names as rocprofv3 demangles them ("k_persist_sort<112, 8, true>"),
+// for rtw_scene_query and the bench's PMC bookkeeping.
+std::string kname(const char* k, int f, int m, int lds = -1, int lst = -1) {
+    std::string s = std::string(k) + "<" + std::to_string(f);
+    if (m >= 0) s += ", " + std::to_string(m);
+    if (lds >= 0) s += lds ? ", true" : ", false";
+    if (lst >= 0) s += lst ? ", true" : ", false";
+    return s + ">";
+}
+
 // Fused traversal + shading for the common scene shapes; returns false when
 // no fused instantiation covers (features, material set), and the caller
-// then runs the split k_intersect / k_shade pair.  probe: only report.
+// then runs the split k_intersect / k_shade pair.  probe: only report (and
+// name the kernel in *name when given).
 bool launch_segment(bool probe, int f, int mask, int grid, hipStream_t st, const scene& S, const job_t& J,
-                    const paths_t& A, const fresh_t& FR, ctrs_t* C, const char* base, uint32_t bytes) {
+                    const paths_t& A, const fresh_t& FR, ctrs_t* C, const char* base, uint32_t bytes,
+                    std::string* name = nullptr) {
     const int pick = pick_shade_mask(mask);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
 #define RTW_SEG(FF, MM, LL)                                                                                    \
     if (f == (FF) && pick == (MM) && lds == (LL)) {                                                          \
+        if (name) *name = kname("k_segment", FF, MM, LL);                                                    \
         if (!probe)                                                                                           \
             hipLaunchKernelGGL((k_segment<FF, MM, LL>), dim3(grid), dim3(kBlock), shm, st, S, J, A, FR, C, base, bytes); \
         return true;                                                                                         \
@@ -1569,28 +1589,41 @@ int persist_sort_grid(size_t shm, int cus) {
 // random_balls flat +12 %, Book-2 flat +37 % with regrouping; random_balls
 // BVH -8 %, Book-2 BVH -2 %: divergent BVH walks dominate there and the
 // per-iteration block barriers cost).  RTW_SORT=0/1 forces either (A/B, tests).
+bool sort_forced(bool& value) {
+    const char* e = std::getenv("RTW_SORT");
+    if (!(e && *e)) return false;
+    value = std::atoi(e) != 0;
+    return true;
+}
+
 template <int FF, int MM, bool LL>
-void launch_pk(int cus, size_t shm, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C, const char* base,
-               uint32_t bytes, int stack_need) {
+void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t st, const scene& S, const job_t& J,
+               ctrs_t* C, const char* base, uint32_t bytes, int stack_need) {
     static const bool sorted = [] {
-        const char* e = std::getenv("RTW_SORT");
-        if (e && *e) return std::atoi(e) != 0;
-        return (FF & (F_WBVH | F_GBVH)) == 0;
+        bool v;
+        return sort_forced(v) ? v : (FF & (F_WBVH | F_GBVH)) == 0;
     }();
-    if (sorted)
-        hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)),
-                           dim3(kSortBlock), shm, st, S, J, C, base, bytes);
-    else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack)
-        hipLaunchKernelGGL((k_persist<FF, MM, LL, true>), dim3(persist_grid<FF, MM, LL, true>(shm, cus)),
-                           dim3(kBlock), shm, st, S, J, C, base, bytes);
-    else
-        hipLaunchKernelGGL((k_persist<FF, MM, LL, false>), dim3(persist_grid<FF, MM, LL, false>(shm, cus)),
-                           dim3(kBlock), shm, st, S, J, C, base, bytes);
+    if (sorted) {
+        if (name) *name = kname("k_persist_sort", FF, MM, LL);
+        if (!probe)
+            hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)),
+                               dim3(kSortBlock), shm, st, S, J, C, base, bytes);
+    } else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack) {
+        if (name) *name = kname("k_persist", FF, MM, LL, true);
+        if (!probe)
+            hipLaunchKernelGGL((k_persist<FF, MM, LL, true>), dim3(persist_grid<FF, MM, LL, true>(shm, cus)),
+                               dim3(kBlock), shm, st, S, J, C, base, bytes);
+    } else {
+        if (name) *name = kname("k_persist", FF, MM, LL, false);
+        if (!probe)
+            hipLaunchKernelGGL((k_persist<FF, MM, LL, false>), dim3(persist_grid<FF, MM, LL, false>(shm, cus)),
+                               dim3(kBlock), shm, st, S, J, C, base, bytes);
+    }
 }
 
 bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C,
                     const char* base, uint32_t bytes, int stack_need = kStack, bool ysph = false,
-                    bool static_scene = false, bool lights = false, bool black = false) {
+                    bool static_scene = false, bool lights = false, bool black = false, std::string* name = nullptr) {
     if (ysph && !(f & (F_WBVH | F_MEDIA))) f |= F_YSPH;  // world runs are walked: y-sphere scans
     const int pick = pick_shade_mask(mask);
     // specialised kernels only
@@ -1598,16 +1631,15 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
                    (static_scene && lights && black ? F_BLACK : 0) | (lights ? 0 : F_NOLIGHTS);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
-#define RTW_PER(FF, MM, LL)                                            \
-    if ((f == (FF) || fs == (FF)) && pick == (MM) && lds == (LL)) {  \
-        if (!probe) launch_pk<FF, MM, LL>(cus, shm, st, S, J, C, base, bytes, stack_need); \
-        return true;                                                 \
+#define RTW_PER(FF, MM, LL)                                                                     \
+    if ((f == (FF) || fs == (FF)) && pick == (MM) && lds == (LL)) {                           \
+        launch_pk<FF, MM, LL>(probe, name, cus, shm, st, S, J, C, base, bytes, stack_need);   \
+        return true;                                                                          \
     }
     // specialised: small list scenes whose shading data fit in LDS, and the
     // lambertian / metal / dielectric sets of the Book-1 scene, flat or BVH
     RTW_PER(F_STATIC | F_LIGHTS | F_BLACK, SF_DIEL, true)
     RTW_PER(F_STATIC | F_LIGHTS, SF_DIEL, true)
-    RTW_PER(F_STATIC, SF_DIEL, true)
     RTW_PER(0, SF_DIEL, true)
     RTW_PER(0, SF_METAL | SF_DIEL, true)
     RTW_PER(0, SF_ALL, true)
@@ -1619,10 +1651,10 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
 #undef RTW_PER
     // general: every material / texture, scene read through the caches, one
     // instantiation per traversal feature set (a world BVH never holds media)
-#define RTW_PER(FF)                                                     \
-    if (f == (FF)) {                                                  \
-        if (!probe) launch_pk<FF, SF_ALL, false>(cus, 0, st, S, J, C, base, bytes, stack_need); \
-        return true;                                                  \
+#define RTW_PER(FF)                                                                          \
+    if (f == (FF)) {                                                                       \
+        launch_pk<FF, SF_ALL, false>(probe, name, cus, 0, st, S, J, C, base, bytes, stack_need); \
+        return true;                                                                       \
     }
     RTW_PER(0)
     RTW_PER(F_YSPH)
@@ -1701,7 +1733,28 @@ int validate_desc(const rtw_scene_desc* d) {
         const rtw_prim& P = d->prims[p];
         if (P.type < RTW_PRIM_SPHERE || P.type > RTW_PRIM_RECT_YZ) return rtw_fail(RTW_ERR_INVALID, "bad prim type");
         if (P.material < 0 || P.material >= d->n_materials) return rtw_fail(RTW_ERR_INVALID, "prim material out of range");
-        if (P.entry >= d->n_entries) return rtw_fail(RTW_ERR_INVALID, "prim entry out of range");
+        if (P.entry < -1 || P.entry >= d->n_entries) return rtw_fail(RTW_ERR_INVALID, "prim entry out of range");
+    }
+    // Every prim of an entry's range names that entry (hit_record reads the
+    // winner's transforms and flips through prims[i].entry), and every prim
+    // outside all ranges -- a light's own copy -- names none: traversal never
+    // returns it, and a prim claimed by two ranges cannot name both.
+    {
+        std::vector<int> owner(d->n_prims, -1);
+        for (int e = 0; e < d->n_entries; ++e) {
+            const rtw_entry& E = d->entries[e];
+            for (int i = E.first_prim; i < E.first_prim + E.n_prims; ++i) {
+                if (owner[i] != -1)
+                    return rtw_fail(RTW_ERR_INVALID, "prim " + std::to_string(i) + " belongs to entries " +
+                                                         std::to_string(owner[i]) + " and " + std::to_string(e));
+                owner[i] = e;
+            }
+        }
+        for (int p = 0; p < d->n_prims; ++p)
+            if (d->prims[p].entry != owner[p])
+                return rtw_fail(RTW_ERR_INVALID, "prim " + std::to_string(p) + " names entry " +
+                                                     std::to_string(d->prims[p].entry) + " but lies in entry " +
+                                                     std::to_string(owner[p]) + "'s range");
     }
     for (int m = 0; m < d->n_materials; ++m) {
         const rtw_material& M = d->materials[m];
@@ -1727,6 +1780,37 @@ int validate_desc(const rtw_scene_desc* d) {
                         : (N.left < 0 || N.left >= d->n_bvh_nodes || N.right < 0 || N.right >= d->n_bvh_nodes))
             return rtw_fail(RTW_ERR_INVALID, "bvh node out of range");
     }
+    // Each BVH is a tree (no node reached twice, so walks terminate and the
+    // upload's depth count is finite) whose leaf items lie in its domain:
+    // prims of the entry's own range (group BVH) or entry indices (world).
+    {
+        std::vector<int> seen(d->n_bvh_nodes, 0);
+        auto walk = [&](int root, int lo, int hi, const char* what) -> int {
+            std::vector<int> todo{root};
+            while (!todo.empty()) {
+                const int n = todo.back();
+                todo.pop_back();
+                if (seen[n]++) return rtw_fail(RTW_ERR_INVALID, std::string(what) + " BVH is not a tree");
+                const rtw_bvh_node& N = d->bvh_nodes[n];
+                if (N.count == 0) {
+                    todo.push_back(N.left);
+                    todo.push_back(N.right);
+                    continue;
+                }
+                for (int k = N.left; k < N.left + N.count; ++k)
+                    if (d->bvh_items[k] < lo || d->bvh_items[k] >= hi)
+                        return rtw_fail(RTW_ERR_INVALID, std::string(what) + " BVH item out of range");
+            }
+            return RTW_OK;
+        };
+        for (int e = 0; e < d->n_entries; ++e) {
+            const rtw_entry& E = d->entries[e];
+            if (E.bvh_root < 0) continue;
+            if (int rc = walk(E.bvh_root, E.first_prim, E.first_prim + E.n_prims, "group")) return rc;
+        }
+        if (d->world_bvh_root >= 0)
+            if (int rc = walk(d->world_bvh_root, 0, d->n_entries, "world")) return rc;
+    }
     return RTW_OK;
 }
 
@@ -1747,7 +1831,94 @@ size_t pass_budget_samples() {
     return size_t(1) << 30;  // 24 GiB of per-sample radiance records per pass (T: one pass)
 }
 
+// The traversal kernel a render of `h` launches under the current
+// environment (RTW_MODE / RTW_SPLIT / RTW_SORT), named as rocprofv3 does.
+std::string render_kernel_name(const handle_t* h) {
+    std::string name;
+    const job_t J{};
+    const char* mode_env = std::getenv("RTW_MODE");
+    const bool wavefront = mode_env && std::string(mode_env) == "wavefront";
+    if (!wavefront && launch_persist(true, h->features, h->shade_mask, 0, nullptr, h->S, J, nullptr, h->scene_base,
+                                     h->shade_bytes, h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0,
+                                     h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL,
+                                     &name))
+        return name;
+    const char* split_env = std::getenv("RTW_SPLIT");
+    const paths_t A{};
+    const fresh_t FR{};
+    if (!(split_env && std::atoi(split_env) != 0) &&
+        launch_segment(true, h->features, h->shade_mask, 0, nullptr, h->S, J, A, FR, nullptr, h->scene_base,
+                       h->shade_bytes, &name))
+        return name;
+    return kname("k_intersect", h->features, -1);
+}
+
+// PPM channel bytes (RayTracingWeekend.cpp:266-270): int(255.99f * c) as
+// x86 converts (truncation; NaN / out of range -> INT_MIN, cvttsd2si).
+__global__ __launch_bounds__(kBlock) void k_quantize(const double* __restrict__ canvas, size_t n,
+                                                     int32_t* __restrict__ out) {
+    for (size_t k = blockIdx.x * (size_t)kBlock + threadIdx.x; k < n; k += (size_t)gridDim.x * kBlock) {
+        const double x = (double)255.99f * canvas[k];
+        out[k] = (x == x && x < 2147483648.0 && x > -2147483649.0) ? (int32_t)x : (int32_t)0x80000000u;
+    }
+}
+
+// dst += src (rtw_render_multi's final add into a device accumulator)
+__global__ __launch_bounds__(kBlock) void k_add(double* __restrict__ dst, const double* __restrict__ src, size_t n) {
+    for (size_t k = blockIdx.x * (size_t)kBlock + threadIdx.x; k < n; k += (size_t)gridDim.x * kBlock)
+        dst[k] += src[k];
+}
+
+unsigned grid_for(size_t n) { return (unsigned)std::max<size_t>(1, std::min<size_t>((n + kBlock - 1) / kBlock, 8192)); }
+
 }  // namespace
+
+#ifndef RTW_BUILD_ID
+#define RTW_BUILD_ID "unknown"
+#endif
+extern "C" const char* rtw_build_id(void) { return RTW_BUILD_ID; }
+
+extern "C" int rtw_scene_query(void* handle, rtw_scene_info* out) {
+    const handle_t* h = static_cast<const handle_t*>(handle);
+    if (!h || !out) return rtw_fail(RTW_ERR_INVALID, "rtw_scene_query: null argument");
+    std::memset(out, 0, sizeof *out);
+    out->device = h->device;
+    out->n_world_runs = h->n_runs;
+    out->n_ysphere_runs = h->n_ysph_runs;
+    out->n_plain_runs = h->n_plain_runs;
+    out->features = h->features;
+    out->shade_mask = h->shade_mask;
+    out->shade_lds_bytes = h->shade_bytes <= kShadeLdsMax ? (int32_t)h->shade_bytes : 0;
+    out->bvh_lds_nodes = 0;
+    const std::string k = render_kernel_name(h);
+    std::snprintf(out->kernel, sizeof out->kernel, "%s", k.c_str());
+    std::snprintf(out->build_id, sizeof out->build_id, "%s", RTW_BUILD_ID);
+    return RTW_OK;
+}
+
+extern "C" int rtw_quantize_canvas_device(void* handle, const double* canvas, int nx, int ny, int32_t* out) {
+    handle_t* h = static_cast<handle_t*>(handle);
+    if (!h || !canvas || !out || nx <= 0 || ny <= 0)
+        return rtw_fail(RTW_ERR_INVALID, "rtw_quantize_canvas_device: bad argument");
+    HIPCHK(hipSetDevice(h->device));
+    const size_t n = (size_t)nx * (size_t)ny * 3;
+    hipLaunchKernelGGL(k_quantize, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, canvas, n, out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return RTW_OK;
+}
+
+// internal (rtw_host_util.h): the device of a handle, and dst += src on it
+int rtw_handle_device(void* handle) { return handle ? static_cast<handle_t*>(handle)->device : -1; }
+
+int rtw_handle_add_device(void* handle, double* dst, const double* src, size_t n) {
+    handle_t* h = static_cast<handle_t*>(handle);
+    HIPCHK(hipSetDevice(h->device));
+    hipLaunchKernelGGL(k_add, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, dst, src, n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return RTW_OK;
+}
 
 extern "C" int rtw_device_count(void) {
     int n = 0;

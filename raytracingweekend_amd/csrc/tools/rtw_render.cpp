@@ -4,7 +4,11 @@
 // P3 PPM, report Trace/Write milliseconds.
 //
 //   rtw_render [--scene cornell_box] [--nx 400] [--ny 400] [--spp 64]
-//              [--depth 100] [--seed 0] [--bvh] [--device 0] [--out out.ppm]
+//              [--depth 100] [--seed 0] [--bvh] [--device 0] [--gpus 1]
+//              [--out out.ppm]
+//
+// --gpus N renders on devices device .. device+N-1 from this one process
+// (rtw_render_multi: one host thread per GPU, RCCL reduce to the first).
 //
 // Defaults are the reference's compile-time constants (RayTracingWeekend.cpp:32-43,
 // scene typedef :201).
@@ -19,7 +23,7 @@
 
 int main(int argc, char** argv) {
     std::string scene_name = "cornell_box", out = "1.ppm";
-    int nx = 400, ny = 400, spp = 64, depth = 100, device = 0, bvh = 0;
+    int nx = 400, ny = 400, spp = 64, depth = 100, device = 0, bvh = 0, gpus = 1;
     unsigned long long seed = 0;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -37,6 +41,7 @@ int main(int argc, char** argv) {
         else if (a == "--depth") depth = std::atoi(next());
         else if (a == "--seed") seed = std::strtoull(next(), nullptr, 10);
         else if (a == "--device") device = std::atoi(next());
+        else if (a == "--gpus") gpus = std::atoi(next());
         else if (a == "--out") out = next();
         else if (a == "--bvh") bvh = 1;
         else {
@@ -55,11 +60,16 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "flatten: %s\n", rtw_last_error());
         return 1;
     }
-    void* h = nullptr;
-    if (rtw_scene_upload(device, desc, &h) != RTW_OK) {
-        std::fprintf(stderr, "upload: %s\n", rtw_last_error());
-        return 1;
+    if (gpus < 1 || device < 0 || device + gpus > rtw_device_count()) {
+        std::fprintf(stderr, "--device %d --gpus %d: only %d devices visible\n", device, gpus, rtw_device_count());
+        return 2;
     }
+    std::vector<void*> h(gpus, nullptr);
+    for (int g = 0; g < gpus; ++g)
+        if (rtw_scene_upload(device + g, desc, &h[g]) != RTW_OK) {
+            std::fprintf(stderr, "upload: %s\n", rtw_last_error());
+            return 1;
+        }
     const rtw_camera_desc cam = sc->GetCamera().desc();
     rtw_render_params p;
     std::memset(&p, 0, sizeof p);
@@ -67,7 +77,9 @@ int main(int argc, char** argv) {
     std::vector<double> accum((size_t)nx * ny * 3, 0.0), canvas(accum.size());
     rtw_stats st;
     auto t0 = std::chrono::high_resolution_clock::now();
-    if (rtw_render_accumulate(h, &cam, &p, accum.data(), &st) != RTW_OK) {
+    const int rc = gpus == 1 ? rtw_render_accumulate(h[0], &cam, &p, accum.data(), &st)
+                             : rtw_render_multi(gpus, h.data(), &cam, &p, accum.data(), &st);
+    if (rc != RTW_OK) {
         std::fprintf(stderr, "render: %s\n", rtw_last_error());
         return 1;
     }
@@ -84,7 +96,8 @@ int main(int argc, char** argv) {
     std::printf("Msamples/s: %.3f  segments/sample: %.4f\n",
                 (double)st.samples / (std::chrono::duration<double>(t1 - t0).count() * 1e6),
                 (double)st.segments / (double)st.samples);
-    rtw_scene_free(h);
+    for (void* x : h) rtw_scene_free(x);
+    if (gpus > 1) rtw_release_communicators();
     rtw_scene_desc_free(desc);
     return 0;
 }

@@ -109,6 +109,27 @@ class DeviceScene:
                                                C.c_void_p(canvas.data_ptr())), "rtw_finalize_canvas_device")
         return canvas
 
+    def query(self) -> dict:
+        """rtw_scene_query: run layout, feature bits, the traversal kernel a
+        render launches now and the device code's build id."""
+        info = _abi.rtw_scene_info()
+        check(lib().rtw_scene_query(self.handle, C.byref(info)), "rtw_scene_query")
+        return info.as_dict()
+
+    def quantize_device(self, canvas, nx: int, ny: int, out=None):
+        """PPM channel values int(255.99f * c) of a device canvas, on the GPU
+        (rtw_quantize_canvas_device).  Returns an int32 CUDA tensor."""
+        import torch
+        if not (canvas.is_cuda and canvas.dtype == torch.float64 and canvas.numel() == nx * ny * 3
+                and canvas.is_contiguous()):
+            raise ValueError("canvas must be a contiguous float64 CUDA tensor of nx*ny*3")
+        if out is None:
+            out = torch.empty(nx * ny * 3, dtype=torch.int32, device=canvas.device)
+        torch.cuda.synchronize(canvas.device)
+        check(lib().rtw_quantize_canvas_device(self.handle, C.c_void_p(canvas.data_ptr()), nx, ny,
+                                               C.c_void_p(out.data_ptr())), "rtw_quantize_canvas_device")
+        return out
+
     def close(self):
         if self.handle:
             lib().rtw_scene_free(self.handle)
@@ -119,6 +140,48 @@ class DeviceScene:
             self.close()
         except Exception:
             pass
+
+
+def render_multi(scenes, nx: int, ny: int, spp: int, max_depth: int, seed: int = 0, *, spp_begin: int = 0,
+                 spp_count: int = 0, row_begin: int = 0, row_step: int = 1, accum=None,
+                 camera: Optional[_abi.rtw_camera_desc] = None, collect_kernel_times: bool = False):
+    """rtw_render_multi over DeviceScenes on distinct GPUs (one process, one
+    host thread per GPU, RCCL reduce to scenes[0]'s device).  `accum`: float64
+    numpy array, or torch float64 tensor on scenes[0]'s device."""
+    if accum is None:
+        accum = np.zeros(nx * ny * 3, dtype=np.float64)
+    on_device = 0
+    if isinstance(accum, np.ndarray):
+        if accum.dtype != np.float64 or accum.size != nx * ny * 3 or not accum.flags["C_CONTIGUOUS"]:
+            raise ValueError("accum must be a contiguous float64 array of nx*ny*3")
+        ptr = accum.ctypes.data_as(C.c_void_p)
+    else:
+        import torch
+        if accum.dtype != torch.float64 or accum.numel() != nx * ny * 3 or not accum.is_contiguous():
+            raise ValueError("accum must be a contiguous float64 tensor of nx*ny*3")
+        torch.cuda.synchronize(accum.device)
+        ptr = C.c_void_p(accum.data_ptr())
+        on_device = 1
+    handles = (C.c_void_p * len(scenes))(*[s.handle.value for s in scenes])
+    prm = _abi.rtw_render_params(nx=nx, ny=ny, spp=spp, max_depth=max_depth, seed=seed, spp_begin=spp_begin,
+                                 spp_count=spp_count, row_begin=row_begin, row_step=row_step,
+                                 accum_on_device=on_device, collect_kernel_times=int(collect_kernel_times),
+                                 wavefront_paths=0, reserved=0)
+    st = _abi.rtw_stats()
+    cam = camera if camera is not None else scenes[0].scene.camera
+    check(lib().rtw_render_multi(len(scenes), handles, C.byref(cam), C.byref(prm), ptr, C.byref(st)),
+          "rtw_render_multi")
+    return accum, st.as_dict()
+
+
+def write_ppm_quantized(path: str, rgb: np.ndarray, nx: int, ny: int) -> None:
+    q = np.ascontiguousarray(rgb, dtype=np.int32)
+    check(lib().rtw_write_ppm_quantized(str(path).encode(), q.ctypes.data_as(C.c_void_p), nx, ny),
+          "rtw_write_ppm_quantized")
+
+
+def build_id() -> str:
+    return lib().rtw_build_id().decode()
 
 
 def device_count() -> int:

@@ -86,9 +86,11 @@ public:
         for (int k = 0; k < 6; ++k)
             Add(mover(vec3(-2.5 + k, 0.3, 1.5), vec3(-2.5 + k, 0.3 + 0.1 * k, 1.5), 0.3, k & 1 ? red : white, 0.0, 1.0));
         Add(std::make_shared<sphere>(vec3(1.7, 0.4, -0.6), 0.4, glass));
-        // a light between the runs
+        // a light between the runs: translated (by zero, which moves nothing)
+        // so that it is not a plain entry -- a flip alone folds into the prim
+        // and would merge run 1, the lamp and run 2 into one mixed run
         auto lamp = std::make_shared<xz_rect>(-1.0, 1.0, -1.0, 1.0, 4.0, light);
-        Add(std::make_shared<flip_normals>(lamp));
+        Add(std::make_shared<translate>(std::make_shared<flip_normals>(lamp), vec3(0.0, 0.0, 0.0)));
         lights->objects.push_back(lamp);
         // run 2: a static sphere at y == 0, an x-mover, a y-mover at x == 0,
         // movers on another interval
@@ -108,7 +110,8 @@ public:
     }
 };
 
-static int check_scene(const scene& us, const char* name, int nx, int ny, int spp, int depth, uint64_t seed) {
+static int check_scene(const scene& us, const char* name, int nx, int ny, int spp, int depth, uint64_t seed,
+                       int min_ysphere_runs = 0) {
     int failures = 0;
     for (int bvh = 0; bvh <= 1; ++bvh) {
         rtw_scene_desc* d = nullptr;
@@ -120,6 +123,16 @@ static int check_scene(const scene& us, const char* name, int nx, int ny, int sp
         if (rtw_scene_upload(0, d, &h) != RTW_OK) {
             std::printf("upload failed: %s\n", rtw_last_error());
             return 1;
+        }
+        rtw_scene_info info;
+        if (rtw_scene_query(h, &info) != RTW_OK) {
+            std::printf("query failed: %s\n", rtw_last_error());
+            return 1;
+        }
+        if (!bvh && info.n_ysphere_runs < min_ysphere_runs) {
+            std::printf("%s: %d y-sphere runs, expected >= %d (run layout %d runs, %d plain)\n", name,
+                        info.n_ysphere_runs, min_ysphere_runs, info.n_world_runs, info.n_plain_runs);
+            ++failures;
         }
         const rtw_camera_desc cam = us.GetCamera().desc();
         rtw_render_params p;
@@ -159,7 +172,7 @@ int main() {
     }
     {
         motion_scene ms(nx * 1.0 / ny);
-        failures += check_scene(ms, "motion", nx, ny, spp, depth, 11);
+        failures += check_scene(ms, "motion", nx, ny, spp, depth, 11, 1);
     }
     std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
     return failures ? 1 : 0;

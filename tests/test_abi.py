@@ -23,7 +23,7 @@ def declared_functions():
 def test_every_declared_symbol_is_exported(built):
     lib = _abi.lib()
     names = declared_functions()
-    assert len(names) == 12
+    assert len(names) == 18
     for n in names:
         assert hasattr(lib, n), f"{n} declared in rtw_gpu.h but not exported"
     nm = subprocess.run(["nm", "-D", "--defined-only", str(_abi.LIB_PATH)], capture_output=True, text=True).stdout
@@ -33,7 +33,7 @@ def test_every_declared_symbol_is_exported(built):
 
 
 STRUCTS = ["rtw_prim", "rtw_entry", "rtw_bvh_node", "rtw_material", "rtw_texture", "rtw_light", "rtw_camera_desc",
-           "rtw_scene_desc", "rtw_render_params", "rtw_stats"]
+           "rtw_scene_desc", "rtw_render_params", "rtw_stats", "rtw_scene_info"]
 
 
 def test_struct_layouts_match_c(tmp_path):

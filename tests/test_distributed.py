@@ -1,6 +1,7 @@
-"""N > 1 path on CPU: world_size-2 gloo ranks run render_sharded with the
-oracle standing in for each rank's GPU renderer (test-only injection), and the
-reduced canvas on rank 0 equals the single-process render."""
+"""N > 1 path on CPU: world_size-2 gloo ranks run bench.py's step
+(raytracingweekend_amd.distributed.render_step) with the oracle standing in
+for each rank's GPU renderer and numpy for the device finalize (test-only
+injection); the reduced canvas on rank 0 equals the single-process render."""
 import os
 import socket
 
@@ -10,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from raytracingweekend_amd.distributed import render_sharded, sample_range
+from raytracingweekend_amd.distributed import render_sharded, render_step, sample_range
 
 NX, NY, SPP, DEPTH, SEED = 20, 16, 5, 50, 3
 
@@ -49,13 +50,27 @@ def _worker(rank, world, port, mode, q):
     from raytracingweekend_amd.render import SceneDesc
     sd = SceneDesc("cornell_box", NX / NY)
     accum = torch.zeros(NX * NY * 3, dtype=torch.float64)
-    canvas = render_sharded(_oracle_fn(sd), NX, NY, SPP, accum, mode=mode)
+    if mode == "step":
+        # bench.py's step: render_step with a finalize into a canvas tensor
+        from oracle_lib import finalize_np
+        canvas_t = torch.full((NX * NY * 3,), -1.0, dtype=torch.float64)
+
+        def fin(acc, canvas):
+            canvas.copy_(torch.from_numpy(finalize_np(acc.numpy(), SPP)))
+
+        for _ in range(2):  # a warmup step and a timed one: the accumulator restarts from zero
+            render_step(_oracle_fn(sd), fin, accum, canvas_t, NX, NY, SPP)
+        canvas = canvas_t.numpy() if rank == 0 else None
+        if rank != 0:
+            assert canvas_t[0] == -1.0  # only rank 0 finalises
+    else:
+        canvas = render_sharded(_oracle_fn(sd), NX, NY, SPP, accum, mode=mode)
     if rank == 0:
         q.put(canvas)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["spp", "rows"])
+@pytest.mark.parametrize("mode", ["spp", "rows", "step"])
 def test_two_rank_gloo_matches_single(built, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
