@@ -161,7 +161,7 @@ def test_device_quantize_and_ppm_bytes(gpu, tmp_path):
     gpu.write_ppm(tmp_path / "a.ppm", c, nx, ny)
     gpu.write_ppm_quantized(tmp_path / "b.ppm", q, nx, ny)
     assert (tmp_path / "a.ppm").read_bytes() == (tmp_path / "b.ppm").read_bytes()
-    assert q[0] == -2147483648 and q[1] == 0 and q[2] == 255 and q[3] == 255
+    assert q[0] == -2147483648 and q[1] == -127 and q[2] == 255 and q[3] == 255  # int() truncates toward 0
 
 
 def test_scene_query_names_the_launched_kernel(gpu):
