@@ -1017,12 +1017,34 @@ RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
     return 0.0;  // hittable.h:36
 }
 
+// The frame (onb::build_from_w(normal), onb.h:32-38) of a lambertian hit,
+// kept as what it is built from and built only where it is used: a rect's
+// world normal is fixed, so its frame comes from the host-built table
+// (scene::prim_onb, same arithmetic); anything else's from its normal.  The
+// 18 registers of a built frame are then never live across the light
+// sampling and the pdfs.
+struct surf_frame {
+    d3 n;
+    int32_t prim;
+    bool rect;
+};
+RTW_D onb frame_onb(const scene& S, const surf_frame& s) {
+    if (s.rect) {
+        const double* f = S.prim_onb + 9 * (size_t)s.prim;
+        return onb{ld3(f), ld3(f + 3), ld3(f + 6)};
+    }
+    return onb_from_w(s.n);
+}
+RTW_D d3 frame_w(const scene& S, const surf_frame& s) {  // == frame_onb(S, s).w
+    return s.rect ? ld3(S.prim_onb + 9 * (size_t)s.prim + 6) : normalize(s.n);
+}
+
 // mixture_pdf(cosine_pdf(n), hittable_pdf(lights, o))::generate (pdf.h:55-79)
 // as one code path: the cosine lobe (utility.h:54-67) and a sphere light
 // (sphere.h:101-108, utility.h:69-81) share their sqrt / sincos / onb tail,
 // so a wave whose lanes took different branches pays for one sincos, not
 // two.  Every lane draws and rounds exactly as its own branch would.
-RTW_D d3 mixture_generate(const scene& S, const onb& uvw, d3 o, uint32_t& rng) {
+RTW_D d3 mixture_generate(const scene& S, const surf_frame& sf, d3 o, uint32_t& rng) {
     const bool cosine = rnd01(rng) < 0.5;
     rtw_light L{RTW_LIGHT_DEFAULT, 0};
     int kind = -1;  // the cosine lobe
@@ -1040,13 +1062,14 @@ RTW_D d3 mixture_generate(const scene& S, const onb& uvw, d3 o, uint32_t& rng) {
         return d3{rx, q.p[4], rz} - o;
     }
     const bool sph = kind == RTW_LIGHT_SPHERE;
-    onb basis = uvw;
+    surf_frame bf = sf;  // the lobe's frame: the surface's, or the light direction's
     double a1 = 1 - r2;
     if (sph) {
         const rtw_prim& q = S.prims[L.prim];
         const d3 direction = ld3(q.p) - o;
         const double distance_squared = len2(direction);
-        basis = onb_from_w(direction);
+        bf.n = direction;
+        bf.rect = false;
         a1 = 1 - q.p[9] / distance_squared;  // radius * radius / distance_squared
     }
     const double s1 = __builtin_sqrt(a1);
@@ -1055,7 +1078,7 @@ RTW_D d3 mixture_generate(const scene& S, const onb& uvw, d3 o, uint32_t& rng) {
     const double phi = kTwoPi * r1;
     double sp, cp;
     sincos_azimuth(phi, sp, cp);
-    return local(basis, d3{cp * sq, sp * sq, z});
+    return local(frame_onb(S, bf), d3{cp * sq, sp * sq, z});
 }
 
 RTW_D double lights_pdf_value(const scene& S, d3 o, d3 v) {  // hittable_list.h:44-53

@@ -321,23 +321,65 @@ struct path_st {
     uint32_t rng, depth, q;
 };
 
-// Outcome of one segment: the path continues with throughput *= f, or ends
-// with radiance thr * E, or ends with radiance 0.
+// Outcome of one segment: the path continues with throughput *= f and the
+// next call's ray, or ends with radiance thr * E, or ends with radiance 0.
 enum { SEG_CONTINUE = 0, SEG_END = 1, SEG_END_ZERO = 2 };
 
+// A sink receives the outcome inside the shading branch that produced it:
+//   cont(f, next)   the path continues (throughput *= f, ray `next`)
+//   end(E)          it ends with radiance thr * E
+//   end_zero()      it ends with radiance 0
+// seg_out keeps the outcome for the caller (wavefront kernels); the
+// persistent kernels' sinks apply it on the spot (LDS throughput update,
+// continuation ray into the path's slot, radiance store), so no value of a
+// branch is live across the merge of the exec-masked branches, which run
+// one after the other.
+struct seg_out {
+    d3 w;      // f or E
+    ray next;  // SEG_CONTINUE only
+    RTW_D void cont(const d3& f, const ray& nr) { w = f, next = nr; }
+    RTW_D void end(const d3& E) { w = E; }
+    RTW_D void end_zero() {}
+};
+template <class C, class E, class Z>
+struct fn_sink {  // a sink from three callables
+    C c;
+    E e;
+    Z z;
+    RTW_D void cont(const d3& f, const ray& nr) { c(f, nr); }
+    RTW_D void end(const d3& L) { e(L); }
+    RTW_D void end_zero() { z(); }
+};
+template <class C, class E, class Z>
+RTW_D fn_sink<C, E, Z> make_sink(C c, E e, Z z) { return fn_sink<C, E, Z>{c, e, z}; }
+
 // One segment of color() (RayTracingWeekend.cpp:52-159) for path x whose
-// world hit is (t, prim).  The recursion's inside-out products are folded
-// forward: the radiance of a path is thr * (last emitted / background), thr
-// the product of the reference's per-bounce factors attenuation *
-// scattering_pdf / pdf (or attenuation for specular scatter).
-template <int M, bool STATIC = false, bool LIGHTS = false, bool BLACK = false, bool NOLIGHTS = false>
-__device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, int32_t prim, d3& E, d3& f,
+// world hit is (t, prim); returns the outcome (SEG_*) after handing it to
+// the sink.  x.r is only read; on SEG_CONTINUE x.rng and x.depth advance.
+// The recursion's inside-out products are folded forward: the radiance of a
+// path is thr * (last emitted / background), thr the product of the
+// reference's per-bounce factors attenuation * scattering_pdf / pdf (or
+// attenuation for specular scatter).
+template <int M, bool STATIC = false, bool LIGHTS = false, bool BLACK = false, bool NOLIGHTS = false, class SINK>
+__device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, int32_t prim, SINK& sk,
                                           prof_t& pf) {
     const ray r = x.r;
     uint32_t rng = x.rng;
     const uint32_t depth = x.depth;
+    // the scattered branches' common tail: the next color() call has depth
+    // depth - 1, and returns 0 when that is 0
+    auto scatter = [&](const d3& f, const d3& p, const d3& dir) -> int {
+        if (depth <= 1) {
+            sk.end_zero();
+            return SEG_END_ZERO;
+        }
+        sk.cont(f, ray{p, dir, r.t});
+        x.rng = rng;
+        x.depth = depth - 1;
+        return SEG_CONTINUE;
+    };
     if (prim == -1) {
-        E = BLACK ? d3{0, 0, 0} : background(S, r.d);
+        sk.end(BLACK ? d3{0, 0, 0} : background(S, r.d));
         return SEG_END;
     }
     d3 p, n;
@@ -345,20 +387,22 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
     bool rect;
     hit_record<(M & SF_ISO) != 0, STATIC>(S, r, hit_state{t, prim, false}, p, n, mat, rect);
     if (!BLACK && S.render_type == RTW_RENDER_NORMAL) {  // :135-136
-        E = d3{0.5f, 0.5f, 0.5f} * (n + d3{1, 1, 1});
+        sk.end(d3{0.5f, 0.5f, 0.5f} * (n + d3{1, 1, 1}));
         return SEG_END;
     }
     const rtw_material& m = S.materials[mat];
     pf.mark(PS_HIT);
-    d3 dir;
     if (m.type == RTW_MAT_DIFFUSE_LIGHT) {  // material.h:232-244: no scatter
-        if (!(dot(n, r.d) > 0)) return SEG_END_ZERO;
-        E = texture_value<M>(S, m.texture, p);
+        if (!(dot(n, r.d) > 0)) {
+            sk.end_zero();
+            return SEG_END_ZERO;
+        }
+        sk.end(texture_value<M>(S, m.texture, p));
         return SEG_END;
     } else if ((M & SF_METAL) && m.type == RTW_MAT_METAL) {  // material.h:128-136
         const d3 reflected = reflect(normalize(r.d), n);
-        dir = reflected + random_in_unit_sphere(rng) * m.fuzz;
-        f = ld3(m.albedo);
+        const d3 dir = reflected + random_in_unit_sphere(rng) * m.fuzz;
+        return scatter(ld3(m.albedo), p, dir);
     } else if ((M & SF_DIEL) && m.type == RTW_MAT_DIELECTRIC) {  // material.h:146-222
         d3 outward;
         double ni_over_nt, cosine;
@@ -376,47 +420,45 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
         const d3 reflected = reflect(r.d, n);
         d3 refracted{0, 0, 0};
         const double reflect_prob = refract(r.d, outward, ni_over_nt, refracted) ? schlick_r0(cosine, S.mat_aux[2 * mat + 1]) : 1.0;
-        dir = (rnd01(rng) < reflect_prob) ? reflected : refracted;
-        f = d3{1.0, 1.0, 1.0};
+        const d3 dir = (rnd01(rng) < reflect_prob) ? reflected : refracted;
+        return scatter(d3{1.0, 1.0, 1.0}, p, dir);
     } else if ((M & SF_ISO) && m.type == RTW_MAT_ISOTROPIC) {  // material.h:257-262
-        dir = random_in_unit_sphere(rng);
-        f = texture_value<M>(S, m.texture, p);
+        const d3 dir = random_in_unit_sphere(rng);
+        return scatter(texture_value<M>(S, m.texture, p), p, dir);
     } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
-        // onb::build_from_w(normal) (onb.h:32-38): a rect's world normal is
-        // fixed, so its frame comes from the host-built table (same arithmetic)
-        onb uvw;
-        if (rect) {
-            const double* f = S.prim_onb + 9 * (size_t)prim;
-            uvw.u = ld3(f), uvw.v = ld3(f + 3), uvw.w = ld3(f + 6);
-        } else {
-            uvw = onb_from_w(n);
-        }
+        // onb::build_from_w(normal) (onb.h:32-38), built where it is used
+        const surf_frame sf{n, prim, rect};
         pf.mark(PS_HIT);
-        double pdf_val;
+        d3 dir;
+        double pdf_val, cosine;
         if (LIGHTS || (!NOLIGHTS && S.n_lights > 0)) {  // mixture_pdf(cosine_pdf, hittable_pdf(lights)) pdf.h:55-79
-            dir = mixture_generate(S, uvw, p, rng);
+            dir = mixture_generate(S, sf, p, rng);
             pf.mark(PS_SAMPLE);
-            const double cw = dot(normalize(dir), uvw.w);
+            // both cosines before the light pdfs, so the normal and the frame
+            // are dead while those run (the values are what the reference
+            // computes after them)
+            const d3 ud = normalize(dir);
+            const double cw = dot(ud, frame_w(S, sf));
+            cosine = dot(n, ud);  // material.h:115-119
             const double p0 = (cw <= 0) ? 0 : cw / kPi;
             pdf_val = 0.5 * p0 + 0.5 * lights_pdf_value(S, p, dir);
         } else {
-            dir = local(uvw, random_cosine_direction(rng));
-            const double cw = dot(normalize(dir), uvw.w);
+            dir = local(frame_onb(S, sf), random_cosine_direction(rng));
+            const d3 ud = normalize(dir);
+            const double cw = dot(ud, frame_w(S, sf));
+            cosine = dot(n, ud);  // material.h:115-119
             pdf_val = (cw <= 0) ? 0 : cw / kPi;
         }
-        if (pdf_val <= 0.0) return SEG_END_ZERO;  // :126-127 returns emitted (= 0)
-        const double cosine = dot(n, normalize(dir));  // material.h:115-119
+        if (pdf_val <= 0.0) {  // :126-127 returns emitted (= 0)
+            sk.end_zero();
+            return SEG_END_ZERO;
+        }
         const double spdf = cosine < 0 ? 0 : cosine / kPi;
+        pf.mark(PS_PDF);
         // attenuation = texture value (material.h:98), read only now: it
         // draws nothing, and a late read keeps it out of the busiest registers
-        f = (texture_value<M>(S, m.texture, p) * spdf) / pdf_val;
-        pf.mark(PS_PDF);
+        return scatter((texture_value<M>(S, m.texture, p) * spdf) / pdf_val, p, dir);
     }
-    if (depth <= 1) return SEG_END_ZERO;  // the next color() call has depth 0 and returns 0
-    x.r = ray{p, dir, r.t};
-    x.rng = rng;
-    x.depth = depth - 1;
-    return SEG_CONTINUE;
 }
 
 // The wavefront form: path x (read from pool slot i or, fresh, from staging)
@@ -431,21 +473,23 @@ __device__ __forceinline__ bool shade_one(const scene& S, const job_t& J, const 
     s.depth = x.fresh ? (uint32_t)J.max_depth : x.depth;
     s.q = x.fresh ? FR.qid[x.src] : P.qid[i];
     q = s.q;
-    d3 E, f;
-    const int out = shade_core<M>(S, s, t, prim, E, f, pf);
+    seg_out so;
+    const int out = shade_core<M>(S, s, t, prim, so, pf);
+    const d3 w = so.w;
+    const ray nr = so.next;
     const d3 thr = x.fresh ? d3{1.0, 1.0, 1.0} : d3{P.tr[i], P.tg[i], P.tb[i]};
     if (out == SEG_END) {
-        L = thr * E;
+        L = thr * w;
         return true;
     }
     if (out == SEG_END_ZERO) {
         L = d3{0, 0, 0};
         return true;
     }
-    const d3 nt = thr * f;
-    P.ox[i] = s.r.o.x, P.oy[i] = s.r.o.y, P.oz[i] = s.r.o.z;
-    P.dx[i] = s.r.d.x, P.dy[i] = s.r.d.y, P.dz[i] = s.r.d.z;
-    P.tm[i] = s.r.t;
+    const d3 nt = thr * w;
+    P.ox[i] = nr.o.x, P.oy[i] = nr.o.y, P.oz[i] = nr.o.z;
+    P.dx[i] = nr.d.x, P.dy[i] = nr.d.y, P.dz[i] = nr.d.z;
+    P.tm[i] = nr.t;
     P.tr[i] = nt.x, P.tg[i] = nt.y, P.tb[i] = nt.z;
     P.rng[i] = s.rng;
     P.depth[i] = s.depth;
@@ -585,22 +629,45 @@ struct ray_batch {  // one wave's buffer of generated camera samples (LDS)
 #else
 #define RTW_PERSIST_WAVES(F, M) (((F) & F_BLACK) || (((F) & F_YSPH) && (M) != SF_ALL) ? 5 : 4)
 #endif
+// The persistent kernels' one argument.
+struct persist_args {
+    scene S;
+    job_t J;
+    ctrs_t* C;
+    const char* base;  // the scene allocation; its shading prefix is staged in LDS
+    uint32_t bytes;    // bytes of that prefix
+};
+
+// The persistent kernels' argument, re-read from the kernarg segment (scalar
+// loads through the scalar cache) by each phase of a loop iteration that
+// uses it.  Read once, every scene / job field a persistent loop touches is
+// hoisted into registers held across the whole loop -- some 80 SGPRs, far
+// past the 106 a wave has, so they spill into VGPR lanes and push the paths'
+// own registers out to scratch.  The opaque copy of the segment pointer stops
+// that hoisting: each phase loads what it uses and lets it go.
+__device__ __forceinline__ const persist_args& args_now() {
+    cptr<persist_args> p = (cptr<persist_args>)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const persist_args*)p;
+}
+
 // LST: BVH traversal stacks in LDS (one column per lane) instead of scratch.
 template <int F, int M, bool LDS, bool LST = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
-void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
+void k_persist(persist_args) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kWaves];
     __shared__ ray_batch s_batch[kWaves];
     __shared__ double s_thr[3][kBlock];  // each lane's path throughput
     __shared__ int s_stack[LST ? kLdsStack : 1][kBlock];
+    __shared__ uint32_t s_q[kBlock];     // each lane's sample id
     if (LDS) {
-        const uint4* src = reinterpret_cast<const uint4*>(base);
+        const persist_args& A = args_now();
+        const uint4* src = reinterpret_cast<const uint4*>(A.base);
         uint4* dst = reinterpret_cast<uint4*>(s_scene);
-        for (uint32_t k = threadIdx.x; k < bytes / 16; k += kBlock) dst[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < A.bytes / 16; k += kBlock) dst[k] = src[k];
         __syncthreads();
     }
-    const scene SS = LDS ? lds_scene(S, base, s_scene) : S;
     const uint32_t lane = threadIdx.x & 63;
     ray_batch& B = s_batch[threadIdx.x >> 6];
     const int own = blockIdx.x % kQShards;
@@ -616,6 +683,9 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
             if (!m) break;
             if (bl == bh) {
                 if (!open) break;
+                const persist_args& A = args_now();
+                const job_t& J = A.J;
+                ctrs_t* const C = A.C;
                 // reserve up to 64 ids, own shard first
                 uint32_t left = 64, given = 0, q = 0;
                 bool got = false;
@@ -659,9 +729,9 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
                 const uint32_t k = bl + rank;
                 x.r = ray{d3{B.ox[k], B.oy[k], B.oz[k]}, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
                 x.rng = B.rng[k];
-                x.q = B.q[k];
+                s_q[threadIdx.x] = B.q[k];
                 s_thr[0][threadIdx.x] = 1.0, s_thr[1][threadIdx.x] = 1.0, s_thr[2][threadIdx.x] = 1.0;
-                x.depth = (uint32_t)J.max_depth;
+                x.depth = (uint32_t)args_now().J.max_depth;
             }
             bl += min((uint32_t)__popcll(m), avail);
             __builtin_amdgcn_wave_barrier();
@@ -669,6 +739,8 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
         if (!__any(x.depth != 0)) break;
         pf.mark(PS_LOAD);
         if (x.depth != 0) {
+            const persist_args& A = args_now();
+            const scene& S = A.S;
             hit_state h;
             if constexpr (LST) {
                 lds_stack stk{&s_stack[0][threadIdx.x]};
@@ -678,23 +750,32 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
             }
             pf.mark(PS_TRAVERSE);
             ++segs;
+            const persist_args& A2 = args_now();
+            const scene SS = LDS ? lds_scene(A2.S, A2.base, s_scene) : A2.S;
 #ifdef RTW_PROF
             pf.classify(h.prim == -1 ? 0
                         : 1 + SS.materials[h.prim <= -2 ? SS.entries[-h.prim - 2].phase_material
                                                         : SS.prims[h.prim].material].type);
 #endif
-            d3 E, f;
-            const int out = shade_core<M, false, false, false, (F & F_NOLIGHTS) != 0>(SS, x, h.t, h.prim, E, f, pf);
-            const d3 thr{s_thr[0][threadIdx.x], s_thr[1][threadIdx.x], s_thr[2][threadIdx.x]};
-            if (out == SEG_CONTINUE) {
-                const d3 nt = thr * f;
-                s_thr[0][threadIdx.x] = nt.x, s_thr[1][threadIdx.x] = nt.y, s_thr[2][threadIdx.x] = nt.z;
-            } else {
-                const d3 L = out == SEG_END ? thr * E : d3{0, 0, 0};
-                double* o = J.L + 3 * (size_t)x.q;
+            // the outcome is applied inside the branch that produced it
+            const uint32_t me = threadIdx.x;
+            auto radiance = [&](const d3& L) {
+                double* o = A2.J.L + 3 * (size_t)s_q[me];
                 o[0] = L.x, o[1] = L.y, o[2] = L.z;
+            };
+            ray nr;
+            auto sk = make_sink(
+                [&](const d3& f, const ray& r) {
+                    s_thr[0][me] *= f.x, s_thr[1][me] *= f.y, s_thr[2][me] *= f.z;
+                    nr = r;
+                },
+                [&](const d3& E) { radiance(d3{s_thr[0][me], s_thr[1][me], s_thr[2][me]} * E); },
+                [&]() { radiance(d3{0, 0, 0}); });
+            const int out = shade_core<M, false, false, false, (F & F_NOLIGHTS) != 0>(SS, x, h.t, h.prim, sk, pf);
+            if (out == SEG_CONTINUE)
+                x.r = nr;
+            else
                 x.depth = 0;
-            }
             pf.mark(PS_STORE);
         }
     }
@@ -705,7 +786,7 @@ void k_persist(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
         for (int k = 0; k < kWaves; ++k) t += s_cnt[k];
-        if (t) atomicAdd(&C->segments[blockIdx.x % 8].v, t);
+        if (t) atomicAdd(&args_now().C->segments[blockIdx.x % 8].v, t);
     }
 }
 
@@ -727,7 +808,7 @@ constexpr int kSortBlock = RTW_SORT_BLOCK;  // paths regrouped together (one wor
 constexpr int kSortWaves = kSortBlock / 64;
 template <int F, int M, bool LDS>
 __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
-void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t bytes) {
+void k_persist_sort(persist_args) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_kc[kSortWaves][K_N];  // per wave, lanes per key
     __shared__ uint32_t s_seg[kSortWaves];
@@ -741,18 +822,24 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
     // held in registers across traversal and sort.  A lane whose path ended
     // keeps the record's slot for the camera sample it takes next.
     __shared__ double s_thr[3][kSortBlock];
+    // Between iterations a lane's path record sits in its own exchange slot
+    // (ray, home index, sample id at [tid]); only the engine and the depth
+    // are loop-carried registers.  A loop-carried ray would hold 12 VGPRs
+    // through every shading branch (exec-masked branches run one after the
+    // other, so a value live into any of them is live across all) -- that
+    // is what pushed this kernel past 96 VGPRs into scratch.
+    x_home[threadIdx.x] = threadIdx.x;
     if (LDS) {
-        const uint4* src = reinterpret_cast<const uint4*>(base);
+        const persist_args& A = args_now();
+        const uint4* src = reinterpret_cast<const uint4*>(A.base);
         uint4* dst = reinterpret_cast<uint4*>(s_scene);
-        for (uint32_t k = threadIdx.x; k < bytes / 16; k += kSortBlock) dst[k] = src[k];
-        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < A.bytes / 16; k += kSortBlock) dst[k] = src[k];
     }
-    const scene SS = LDS ? lds_scene(S, base, s_scene) : S;
+    __syncthreads();
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int own = blockIdx.x % kQShards;
     path_st x;
     x.depth = 0;
-    uint32_t home = threadIdx.x;  // this record's s_thr slot
     bool open = true;  // wave-uniform: the queue may still hold samples
     uint32_t segs = 0;
     prof_t pk;  // section profiler (RTW_PROF builds): refill, traverse, sort, exchange, shade
@@ -762,6 +849,9 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
             const bool idle = x.depth == 0;
             const unsigned long long m = __ballot(idle);
             if (open && m) {
+                const persist_args& A = args_now();
+                const job_t& J = A.J;
+                ctrs_t* const C = A.C;
                 const uint32_t want = (uint32_t)__popcll(m);
                 const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
                 uint32_t left = want, given = 0, q = 0;
@@ -787,10 +877,14 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
                 }
                 if (left) open = false;
                 if (got) {
-                    x.r = camera_sample(J, q, x.rng);
-                    if (F & F_STATIC) x.r.t = 0.0;  // never read (F_STATIC)
-                    x.q = q;
+                    const ray r = camera_sample(J, q, x.rng);
+                    const uint32_t me = threadIdx.x;
+                    x_o[0][me] = r.o.x, x_o[1][me] = r.o.y, x_o[2][me] = r.o.z;
+                    x_d[0][me] = r.d.x, x_d[1][me] = r.d.y, x_d[2][me] = r.d.z;
+                    if (!(F & F_STATIC)) x_tm[me] = r.t;  // F_STATIC: never read
+                    x_q[me] = q;
                     x.depth = (uint32_t)J.max_depth;
+                    const uint32_t home = x_home[threadIdx.x];
                     s_thr[0][home] = 1.0, s_thr[1][home] = 1.0, s_thr[2][home] = 1.0;
                 }
             }
@@ -801,7 +895,12 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         int32_t hp = -1;
         int key = K_IDLE;
         if (x.depth != 0) {
-            const hit_state h = world_closest<F>(S, x.r, x.rng);
+            const uint32_t me = threadIdx.x;
+            x.r = ray{d3{x_o[0][me], x_o[1][me], x_o[2][me]}, d3{x_d[0][me], x_d[1][me], x_d[2][me]},
+                      (F & F_STATIC) ? 0.0 : x_tm[me]};
+            const persist_args& A = args_now();
+            const scene SS = LDS ? lds_scene(A.S, A.base, s_scene) : A.S;
+            const hit_state h = world_closest<F>(A.S, x.r, x.rng);
             ++segs;
             th = h.t;
             hp = h.prim;
@@ -818,7 +917,10 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
             }
         }
         pk.mark(PS_TRAVERSE);
-        // 3. counting sort of the block's paths by key
+        // 3. counting sort of the block's paths by key (the record's home and
+        // sample id are read from the lane's own slot before the barrier that
+        // precedes the exchange's writes)
+        const uint32_t my_home = x_home[threadIdx.x], my_q = x_q[threadIdx.x];
         uint32_t rank_in_wave = 0;
         // keys the scene's material set cannot produce are skipped (their
         // counts stay 0; keep s_kc's slots zero for the prefix below)
@@ -850,43 +952,56 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
         }
         if (idle_total == kSortBlock) break;  // block-uniform: nothing left to trace or take
         pk.mark(PS_HIT);
-        // 4. move every path to the slot of its rank
-        x_o[0][dst] = x.r.o.x, x_o[1][dst] = x.r.o.y, x_o[2][dst] = x.r.o.z;
-        x_d[0][dst] = x.r.d.x, x_d[1][dst] = x.r.d.y, x_d[2][dst] = x.r.d.z;
-        if (!(F & F_STATIC)) x_tm[dst] = x.r.t;
-        x_home[dst] = home;
+        // 4. move every path to the slot of its rank (an idle record's ray
+        // is garbage and stays behind)
+        if (x.depth != 0) {
+            x_o[0][dst] = x.r.o.x, x_o[1][dst] = x.r.o.y, x_o[2][dst] = x.r.o.z;
+            x_d[0][dst] = x.r.d.x, x_d[1][dst] = x.r.d.y, x_d[2][dst] = x.r.d.z;
+            if (!(F & F_STATIC)) x_tm[dst] = x.r.t;
+        }
+        x_home[dst] = my_home;
         x_t[dst] = th;
         x_prim[dst] = hp;
         x_rng[dst] = x.rng;
         x_depth[dst] = x.depth;
-        x_q[dst] = x.q;
+        x_q[dst] = my_q;
         __syncthreads();
-        const uint32_t me = threadIdx.x;
-        x.r = ray{d3{x_o[0][me], x_o[1][me], x_o[2][me]}, d3{x_d[0][me], x_d[1][me], x_d[2][me]},
-                  (F & F_STATIC) ? 0.0 : x_tm[me]};
-        home = x_home[me];
-        th = x_t[me];
-        hp = x_prim[me];
+        // (opaque, so the exchange's per-lane LDS addresses are formed here
+        // from one register, not hoisted out of the loop one per array)
+        uint32_t me = threadIdx.x;
+        asm volatile("" : "+v"(me));
         x.rng = x_rng[me];
         x.depth = x_depth[me];
-        x.q = x_q[me];
         pk.mark(PS_SAMPLE);
         // 5. shading, now mostly one branch per wave
         if (x.depth != 0) {
+            x.r = ray{d3{x_o[0][me], x_o[1][me], x_o[2][me]}, d3{x_d[0][me], x_d[1][me], x_d[2][me]},
+                      (F & F_STATIC) ? 0.0 : x_tm[me]};
+            const persist_args& A = args_now();
+            const scene SS = LDS ? lds_scene(A.S, A.base, s_scene) : A.S;
             prof_t pf;
-            d3 E, f;
-            const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0,
-                                       (F & F_NOLIGHTS) != 0>(SS, x, th, hp, E, f, pf);
-            const d3 thr{s_thr[0][home], s_thr[1][home], s_thr[2][home]};
-            if (out == SEG_CONTINUE) {
-                const d3 nt = thr * f;
-                s_thr[0][home] = nt.x, s_thr[1][home] = nt.y, s_thr[2][home] = nt.z;
-            } else {
-                const d3 L = out == SEG_END ? thr * E : d3{0, 0, 0};
-                double* o = J.L + 3 * (size_t)x.q;
+            // the outcome is applied inside the branch that produced it
+            auto radiance = [&](const d3& L) {
+                double* o = A.J.L + 3 * (size_t)x_q[me];
                 o[0] = L.x, o[1] = L.y, o[2] = L.z;
-                x.depth = 0;
-            }
+            };
+            auto sk = make_sink(
+                [&](const d3& f, const ray& nr) {
+                    const uint32_t home = x_home[me];
+                    s_thr[0][home] *= f.x, s_thr[1][home] *= f.y, s_thr[2][home] *= f.z;
+                    // the continuation ray waits in the lane's own slot
+                    x_o[0][me] = nr.o.x, x_o[1][me] = nr.o.y, x_o[2][me] = nr.o.z;
+                    x_d[0][me] = nr.d.x, x_d[1][me] = nr.d.y, x_d[2][me] = nr.d.z;
+                    if (!(F & F_STATIC)) x_tm[me] = nr.t;
+                },
+                [&](const d3& E) {
+                    const uint32_t home = x_home[me];
+                    radiance(d3{s_thr[0][home], s_thr[1][home], s_thr[2][home]} * E);
+                },
+                [&]() { radiance(d3{0, 0, 0}); });
+            const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0,
+                                       (F & F_NOLIGHTS) != 0>(SS, x, x_t[me], x_prim[me], sk, pf);
+            if (out != SEG_CONTINUE) x.depth = 0;
         }
         pk.mark(PS_STORE);
     }
@@ -897,7 +1012,7 @@ void k_persist_sort(scene S, job_t J, ctrs_t* C, const char* base, uint32_t byte
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
         for (int k = 0; k < kSortWaves; ++k) t += s_seg[k];
-        if (t) atomicAdd(&C->segments[blockIdx.x % 8].v, t);
+        if (t) atomicAdd(&args_now().C->segments[blockIdx.x % 8].v, t);
     }
 }
 
@@ -1545,12 +1660,14 @@ bool launch_segment(bool probe, int f, int mask, int grid, hipStream_t st, const
             hipLaunchKernelGGL((k_segment<FF, MM, LL>), dim3(grid), dim3(kBlock), shm, st, S, J, A, FR, C, base, bytes); \
         return true;                                                                                         \
     }
+#ifndef RTW_SUBSET
     RTW_SEG(0, SF_DIEL, true)
     RTW_SEG(0, SF_METAL | SF_DIEL, true)
     RTW_SEG(0, SF_ALL, true)
     RTW_SEG(0, SF_ALL, false)
     RTW_SEG(F_WBVH, SF_ALL, false)
     RTW_SEG(F_WBVH, SF_ALL, true)
+#endif
 #undef RTW_SEG
     return false;
 }
@@ -1607,17 +1724,17 @@ void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t s
         if (name) *name = kname("k_persist_sort", FF, MM, LL);
         if (!probe)
             hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)),
-                               dim3(kSortBlock), shm, st, S, J, C, base, bytes);
+                               dim3(kSortBlock), shm, st, persist_args{S, J, C, base, bytes});
     } else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack) {
         if (name) *name = kname("k_persist", FF, MM, LL, true);
         if (!probe)
             hipLaunchKernelGGL((k_persist<FF, MM, LL, true>), dim3(persist_grid<FF, MM, LL, true>(shm, cus)),
-                               dim3(kBlock), shm, st, S, J, C, base, bytes);
+                               dim3(kBlock), shm, st, persist_args{S, J, C, base, bytes});
     } else {
         if (name) *name = kname("k_persist", FF, MM, LL, false);
         if (!probe)
             hipLaunchKernelGGL((k_persist<FF, MM, LL, false>), dim3(persist_grid<FF, MM, LL, false>(shm, cus)),
-                               dim3(kBlock), shm, st, S, J, C, base, bytes);
+                               dim3(kBlock), shm, st, persist_args{S, J, C, base, bytes});
     }
 }
 
@@ -1638,6 +1755,7 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     }
     // specialised: small list scenes whose shading data fit in LDS, and the
     // lambertian / metal / dielectric sets of the Book-1 scene, flat or BVH
+#ifndef RTW_SUBSET
     RTW_PER(F_STATIC | F_LIGHTS | F_BLACK, SF_DIEL, true)
     RTW_PER(F_STATIC | F_LIGHTS, SF_DIEL, true)
     RTW_PER(0, SF_DIEL, true)
@@ -1648,6 +1766,10 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     RTW_PER(F_YSPH, SF_METAL | SF_DIEL, false)
     RTW_PER(F_WBVH | F_NOLIGHTS, SF_METAL | SF_DIEL, false)
     RTW_PER(F_WBVH, SF_METAL | SF_DIEL, false)
+#else
+    // experiment builds (scripts/ru_kernel.sh): one persistent kernel only
+    RTW_PER(RTW_SUBSET_F, RTW_SUBSET_M, RTW_SUBSET_L)
+#endif
 #undef RTW_PER
     // general: every material / texture, scene read through the caches, one
     // instantiation per traversal feature set (a world BVH never holds media)
@@ -1656,6 +1778,7 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
         launch_pk<FF, SF_ALL, false>(probe, name, cus, 0, st, S, J, C, base, bytes, stack_need); \
         return true;                                                                       \
     }
+#ifndef RTW_SUBSET
     RTW_PER(0)
     RTW_PER(F_YSPH)
     RTW_PER(F_MEDIA)
@@ -1664,6 +1787,7 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     RTW_PER(F_YSPH | F_GBVH)
     RTW_PER(F_MEDIA | F_GBVH)
     RTW_PER(F_WBVH | F_GBVH)
+#endif
 #undef RTW_PER
     return false;
 }
@@ -1678,6 +1802,7 @@ void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_
     case M * 2 + (LDS ? 1 : 0):                                                                            \
         hipLaunchKernelGGL((k_shade<M, LDS>), dim3(grid), dim3(kBlock), shm, st, S, J, A, F, ht, hid, C, base, bytes); \
         break;
+#ifndef RTW_SUBSET
         RTW_CASE(SF_DIEL, true)
         RTW_CASE(SF_DIEL, false)
         RTW_CASE(SF_METAL | SF_DIEL, true)
@@ -1685,6 +1810,7 @@ void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_
         RTW_CASE(SF_NOISE, true)
         RTW_CASE(SF_NOISE, false)
         RTW_CASE(SF_ALL, true)
+#endif
 #undef RTW_CASE
     default:
         hipLaunchKernelGGL((k_shade<SF_ALL, false>), dim3(grid), dim3(kBlock), 0, st, S, J, A, F, ht, hid, C, base, bytes);
@@ -1701,12 +1827,14 @@ void launch_intersect(int f, int grid, hipStream_t st, const scene& S, const pat
     case F:                                                                                       \
         hipLaunchKernelGGL(k_intersect<F>, dim3(grid), dim3(kBlock), 0, st, S, A, FR, ht, hid, C); \
         break;
+#ifndef RTW_SUBSET
         RTW_CASE(0)
         RTW_CASE(F_MEDIA)
         RTW_CASE(F_WBVH)
         RTW_CASE(F_GBVH)
         RTW_CASE(F_MEDIA | F_GBVH)
         RTW_CASE(F_WBVH | F_GBVH)
+#endif
 #undef RTW_CASE
     default:
         hipLaunchKernelGGL(k_intersect<F_MEDIA | F_GBVH>, dim3(grid), dim3(kBlock), 0, st, S, A, FR, ht, hid, C);
