@@ -397,14 +397,77 @@ struct hit_state {
     bool rect;    // winner accepts equal t (for BVH tie order)
 };
 
+// Shared-divisor rect tests (rtw_div.h rcp_hw / div_hw): every rect test of
+// a walk divides by one of the ray's three direction components
+// (t = (k - o.K) / d.K, hittable.h:149-165), so a scan computes the three
+// reciprocals once and each test pays a multiply and two fma instead of a
+// full division -- bit-identical to the division when |d.K| is in
+// [2^-200, 2^200] and the numerator in [2^-800, 2^100]:
+//  * divisor: checked per walk and axis (false for 0, NaN, inf);
+//  * numerator above: scene::fast_div bounds every rect coordinate by 2^40
+//    and the walk checks |o| <= 2^40, so |k - o.K| <= 2^41;
+//  * numerator below 2^-800: both quotients are below 2^-599 and rejected
+//    alike by t < t_min -- so only walks with t_min >= 0.001 (the world
+//    walks; not the media boundary probes) use it.
+// Lanes outside the ranges divide exactly.
+struct rect_rcp {
+    double y[3];
+    bool ok[3];
+};
+RTW_D rect_rcp make_rect_rcp(const scene& S, const ray& r) {
+    constexpr double kB = 0x1p40;
+    const bool base = S.fast_div != 0 && __builtin_fabs(r.o.x) <= kB && __builtin_fabs(r.o.y) <= kB &&
+                      __builtin_fabs(r.o.z) <= kB;
+    rect_rcp q;
+    const double d[3] = {r.d.x, r.d.y, r.d.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        q.y[k] = rcp_hw(d[k]);
+        q.ok[k] = base && div_hw_ok_b(d[k]);
+    }
+    return q;
+}
+// rect_axis_t with the walk's shared reciprocal of d.K
+template <int K, int A, int B>
+RTW_D bool rect_axis_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, double t0, double t1,
+                         double& t_out) {
+    const double ok = K == 0 ? r.o.x : (K == 1 ? r.o.y : r.o.z);
+    const double od = K == 0 ? r.d.x : (K == 1 ? r.d.y : r.d.z);
+    const double num = q.p[4] - ok;
+    double t = div_hw(num, od, rr.y[K]);
+    if (__builtin_expect(!rr.ok[K], 0)) {
+        asm volatile("");  // keeps the exact division behind the branch
+        t = num / od;
+    }
+    if (t < t0 || t > t1) return false;
+    const double a = (A == 0 ? r.o.x : r.o.y) + t * (A == 0 ? r.d.x : r.d.y);
+    const double b = (B == 1 ? r.o.y : r.o.z) + t * (B == 1 ? r.d.y : r.d.z);
+    if (a < q.p[0] || a > q.p[1] || b < q.p[2] || b > q.p[3]) return false;
+    t_out = t;
+    return true;
+}
+RTW_D bool rect_t_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, double t0, double t1, double& t_out) {
+    if (q.type == RTW_PRIM_RECT_XY) return rect_axis_rcp<2, 0, 1>(q, r, rr, t0, t1, t_out);
+    if (q.type == RTW_PRIM_RECT_XZ) return rect_axis_rcp<1, 0, 2>(q, r, rr, t0, t1, t_out);
+    return rect_axis_rcp<0, 1, 2>(q, r, rr, t0, t1, t_out);
+}
+
+#ifndef RTW_RECT_RCP
+#define RTW_RECT_RCP 1
+#endif
+
 // Linear closest hit over prims [first, first+n) of one group, in list order
 // (t range (t_min, closest]) with the reference's own comparisons; the
 // primitive data are wave-uniform scalar loads.
-// (STATIC: the scene has no moving spheres, centres are center0.)
-template <bool STATIC = false>
+// (STATIC: the scene has no moving spheres, centres are center0.  WORLD: a
+// world walk, t_min = 0.001: rect tests share the direction's reciprocals.)
+template <bool STATIC = false, bool WORLD = false>
 RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, bool movers) {
     const double fc = STATIC ? 0.0 : motion_frac(S, r.t, movers);
     const double a = dot(r.d, r.d);  // sphere.h:50, the same for every sphere
+    constexpr bool kRcp = WORLD && RTW_RECT_RCP;
+    rect_rcp rr;
+    if (kRcp) rr = make_rect_rcp(S, r);
     for (int i = 0; i < n; ++i) {
         const rtw_prim q = uprim(S.prims, first + i);
         if (is_sphere(q.type)) {
@@ -430,7 +493,7 @@ RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_m
             }
         } else {
             double t;
-            if (rect_t(q, r, t_min, h.t, t)) {
+            if (kRcp ? rect_t_rcp(q, r, rr, t_min, h.t, t) : rect_t(q, r, t_min, h.t, t)) {
                 h.t = t;
                 h.prim = first + i;
                 h.rect = true;
@@ -880,8 +943,8 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                         continue;
                     }
                 }
-                group_scan<(F & F_STATIC) != 0>(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), lr, kTMin, h,
-                                                ld(&S.runs[ri].movers));
+                group_scan<(F & F_STATIC) != 0, true>(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), lr,
+                                                      kTMin, h, ld(&S.runs[ri].movers));
             }
         }
         if (F & F_MEDIA) {
