@@ -9,6 +9,10 @@ Writes, for the parity tests (which must run where the reference is absent):
   perlin.json            Perlin tables + noise/turb/texture known answers
   render_<case>.npy      per-pixel radiance sums (float64, nx*ny*3)
   renders.json           the cases: scene, size, spp, depth, seed, segments
+  ppm_<case>.ppm         whole images as the reference writes them
+                         (RayTracingWeekend.cpp:235-276: average, gamma 2,
+                         clamp, P3 rows ny-1..0, int(255.99f * c))
+  ppms.json              their cases
 """
 from __future__ import annotations
 
@@ -38,6 +42,12 @@ RENDERS = [
     ("book2_final_16x16x2_d50", "book2_final", 16, 16, 2, 50, 0),
 ]
 
+# whole-image P3 files (case, scene, nx, ny, spp, depth, seed)
+PPMS = [
+    ("cornell_48x48x8_d50", "cornell_box", 48, 48, 8, 50, 0),
+    ("random_balls_60x40x4_d50", "random_balls", 60, 40, 4, 50, 7),
+]
+
 
 def run(*args) -> str:
     r = subprocess.run([str(REF), *map(str, args)], check=True, capture_output=True, text=True)
@@ -64,7 +74,13 @@ def main() -> int:
         meta.append({"case": case, "scene": scene, "nx": nx, "ny": ny, "spp": spp, "max_depth": depth,
                      "seed": seed, "segments": info["segments"]})
     (OUT / "renders.json").write_text(json.dumps(meta, indent=1))
-    print(f"wrote {len(SCENES)} scenes, perlin, {len(RENDERS)} renders to {OUT}")
+    ppm_meta = []
+    for case, scene, nx, ny, spp, depth, seed in PPMS:
+        run("ppm", scene, nx, ny, spp, depth, seed, 8, OUT / f"ppm_{case}.ppm")
+        ppm_meta.append({"case": case, "scene": scene, "nx": nx, "ny": ny, "spp": spp, "max_depth": depth,
+                         "seed": seed})
+    (OUT / "ppms.json").write_text(json.dumps(ppm_meta, indent=1))
+    print(f"wrote {len(SCENES)} scenes, perlin, {len(RENDERS)} renders, {len(PPMS)} ppm images to {OUT}")
     return 0
 
 

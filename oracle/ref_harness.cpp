@@ -35,6 +35,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <chrono>
 #include <map>
 #include <string>
@@ -398,9 +399,37 @@ static void dump_perlin() {
     printf("]}\n");
 }
 
+// The reference's output step for a rendered image, RayTracingWeekend.cpp:
+// 235-244 (average, gamma 2, clamp into the canvas) and 252-276 (P3 header,
+// rows ny-1..0, int(255.99f * c) per channel, streamed with operator<<),
+// over the per-pixel sums of render().
+static int write_ppm_reference(const char* path, const std::vector<double>& sums, int nx, int ny, int spp) {
+    std::vector<vec3> canvas(nx * ny);
+    for (int j = 0; j < ny; j++)
+        for (int i = 0; i < nx; i++) {
+            const double* o = &sums[((size_t)j * nx + i) * 3];
+            vec3 sum(o[0], o[1], o[2]);
+            vec3 col = sum / static_cast<double>(spp);
+            col = vec3(std::min(sqrt(col.x), 1.0), std::min(sqrt(col.y), 1.0), std::min(sqrt(col.z), 1.0));
+            canvas[j * nx + i] = col;
+        }
+    std::ofstream out(path, std::ios::binary);
+    if (!out) return 3;
+    out << "P3\n" << nx << " " << ny << "\n255\n";
+    for (int j = ny - 1; j >= 0; j--)
+        for (int i = 0; i < nx; i++) {
+            vec3 col = canvas[j * nx + i];
+            int ir = int(255.99f * col.r);
+            int ig = int(255.99f * col.g);
+            int ib = int(255.99f * col.b);
+            out << ir << " " << ig << " " << ib << "\n";
+        }
+    return out.good() ? 0 : 3;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
-        fprintf(stderr, "usage: %s scene|render|bench|perlin ...\n", argv[0]);
+        fprintf(stderr, "usage: %s scene|render|bench|perlin|ppm ...\n", argv[0]);
         return 2;
     }
     std::string cmd = argv[1];
@@ -413,7 +442,7 @@ int main(int argc, char** argv) {
         dump_perlin();
         return 0;
     }
-    if ((cmd == "render" && argc == 10) || (cmd == "bench" && argc == 9)) {
+    if ((cmd == "render" && argc == 10) || (cmd == "bench" && argc == 9) || (cmd == "ppm" && argc == 10)) {
         std::string name = argv[2];
         int nx = atoi(argv[3]), ny = atoi(argv[4]), spp = atoi(argv[5]), depth = atoi(argv[6]);
         uint64_t seed = strtoull(argv[7], nullptr, 10);
@@ -428,6 +457,7 @@ int main(int argc, char** argv) {
         double samples = (double)nx * ny * spp;
         printf("{\"seconds\":%.6f,\"samples\":%.0f,\"segments\":%llu,\"msamples_per_s\":%.6f,\"threads\":%d}\n", sec,
                samples, (unsigned long long)segments, samples / sec / 1e6, threads);
+        if (cmd == "ppm") return write_ppm_reference(argv[9], sums, nx, ny, spp);
         if (cmd == "render") {
             FILE* f = fopen(argv[9], "wb");
             if (!f) return 3;
