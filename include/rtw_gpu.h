@@ -39,8 +39,8 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 1
-#define RTW_MAX_OPS 4
+#define RTW_ABI_VERSION 2
+#define RTW_MAX_OPS 8
 
 /* ------------------------------------------------------------------ */
 /* status codes                                                        */
@@ -101,10 +101,14 @@ typedef struct rtw_entry {
     int32_t phase_material; /* MEDIUM: isotropic material index                */
     int32_t bvh_root;       /* -1: linear scan; else root node of a BVH whose
                                items are prim indices of this group           */
+    int32_t n_outer_ops;    /* MEDIUM: ops [0, n_outer_ops) enclose the medium
+                               (its distances are measured in their frame);
+                               the rest belong to its boundary (GROUP: 0)    */
+    int32_t pad;
     double op_param[RTW_MAX_OPS][3];
     double density;         /* MEDIUM                                          */
     double bounds[6];       /* AABB min xyz, max xyz (world space)             */
-} rtw_entry; /* 192 bytes */
+} rtw_entry; /* 312 bytes */
 
 /* BVH node: internal when count == 0 (children left/right), leaf when
  * count > 0 (items bvh_items[left .. left+count)). */
@@ -202,7 +206,19 @@ typedef struct rtw_scene_desc {
     const double* perlin_ranvec; /* 256*3 (noise.h:219) */
     const int32_t* perlin_perm;  /* 3*256 perm_x, perm_y, perm_z (noise.h:221-223) */
     rtw_camera_desc camera;
+    /* Visit program of a scene with media (n_visits > 0): the entries in the
+     * order the reference's world hit calls them -- hittable_list::hit walks
+     * its objects twice (hittable_list.h:16-34), so every list that holds a
+     * constant_medium appears twice, nested lists inside each walk.  Second-
+     * walk visits carry RTW_VISIT_REPLAY; entry index = visit & RTW_VISIT_ENTRY.
+     * n_visits == 0: the world's two walks over entries[0 .. n_entries). */
+    const int32_t* visits;
+    int32_t n_visits;
+    int32_t pad;
 } rtw_scene_desc;
+
+#define RTW_VISIT_REPLAY 0x40000000
+#define RTW_VISIT_ENTRY 0x3fffffff
 
 /* ------------------------------------------------------------------ */
 /* render                                                              */

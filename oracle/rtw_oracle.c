@@ -268,10 +268,10 @@ static void op_rec_out(const rtw_entry* e, int k, hit_rec* rec) {
  * The reference walks nested lists twice (hittable_list.h:16-34); for these
  * deterministic primitives the second walk re-accepts only what the first
  * kept, so one walk gives the same record. */
-static int group_hit(const rtw_scene_desc* S, const rtw_entry* e, const ray* r0, double t_min, double t_max,
-                     hit_rec* rec) {
+static int group_hit_ops(const rtw_scene_desc* S, const rtw_entry* e, int k0, const ray* r0, double t_min,
+                         double t_max, hit_rec* rec) {
     ray r = *r0;
-    for (int k = 0; k < e->n_ops; k++) op_ray_in(e, k, &r);
+    for (int k = k0; k < e->n_ops; k++) op_ray_in(e, k, &r);
     hit_rec tmp;
     int any = 0;
     double closest = t_max;
@@ -283,16 +283,26 @@ static int group_hit(const rtw_scene_desc* S, const rtw_entry* e, const ray* r0,
         }
     }
     if (!any) return 0;
-    for (int k = e->n_ops - 1; k >= 0; k--) op_rec_out(e, k, rec);
+    for (int k = e->n_ops - 1; k >= k0; k--) op_rec_out(e, k, rec);
     return 1;
 }
+static int group_hit(const rtw_scene_desc* S, const rtw_entry* e, const ray* r0, double t_min, double t_max,
+                     hit_rec* rec) {
+    return group_hit_ops(S, e, 0, r0, t_min, t_max, rec);
+}
 
-/* constant_medium::hit hittable.h:430-479 (one call = at most one draw) */
-static int medium_hit(const rtw_scene_desc* S, const rtw_entry* e, const ray* r, double t_min, double t_max,
+/* constant_medium::hit hittable.h:430-479 (one call = at most one draw), in
+ * the frame of the transforms enclosing it (ops [0, n_outer_ops): translate /
+ * rotate_y hand it their moved ray and move its record back out); its
+ * boundary is the rest of the chain over the group. */
+static int medium_hit(const rtw_scene_desc* S, const rtw_entry* e, const ray* rw, double t_min, double t_max,
                       hit_rec* rec, rng* g) {
     hit_rec rec1, rec2;
-    if (group_hit(S, e, r, -DBL_MAX, DBL_MAX, &rec1)) {
-        if (group_hit(S, e, r, rec1.t + 0.0001f, DBL_MAX, &rec2)) {
+    ray rm = *rw;
+    for (int k = 0; k < e->n_outer_ops; k++) op_ray_in(e, k, &rm);
+    const ray* r = &rm;
+    if (group_hit_ops(S, e, e->n_outer_ops, r, -DBL_MAX, DBL_MAX, &rec1)) {
+        if (group_hit_ops(S, e, e->n_outer_ops, r, rec1.t + 0.0001f, DBL_MAX, &rec2)) {
             if (rec1.t < t_min) rec1.t = t_min;
             if (rec2.t > t_max) rec2.t = t_max;
             if (rec1.t >= rec2.t) return 0;
@@ -304,6 +314,7 @@ static int medium_hit(const rtw_scene_desc* S, const rtw_entry* e, const ray* r,
                 rec->p = at(r, rec->t);
                 rec->normal = mk(1, 0, 0);
                 rec->mat = e->phase_material;
+                for (int k = e->n_outer_ops - 1; k >= 0; k--) op_rec_out(e, k, rec);
                 return 1;
             }
         }
@@ -317,11 +328,24 @@ static int entry_hit(const rtw_scene_desc* S, const rtw_entry* e, const ray* r, 
     return group_hit(S, e, r, t0, t1, rec);
 }
 
-/* hittable_list::hit hittable_list.h:11-37 — the world list, walked twice */
+/* hittable_list::hit hittable_list.h:11-37 — the world list, walked twice;
+ * with a visit program (nested lists holding media), the entries in the
+ * order the reference's nested walks call them, replays included */
 static int world_hit(const rtw_scene_desc* S, const ray* r, double t_min, double t_max, hit_rec* rec, rng* g) {
     hit_rec tmp;
     int any = 0;
     double closest = t_max;
+    if (S->n_visits > 0) {
+        for (int k = 0; k < S->n_visits; k++) {
+            const rtw_entry* e = &S->entries[S->visits[k] & RTW_VISIT_ENTRY];
+            if (entry_hit(S, e, r, t_min, closest, &tmp, g)) {
+                any = 1;
+                closest = tmp.t;
+                *rec = tmp;
+            }
+        }
+        return any;
+    }
     for (int pass = 0; pass < 2; pass++) {
         for (int i = 0; i < S->n_entries; i++) {
             if (entry_hit(S, &S->entries[i], r, t_min, closest, &tmp, g)) {

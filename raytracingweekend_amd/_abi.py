@@ -13,8 +13,8 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("RTW_LIBRARY", PKG / "librtw.so"))
 
-RTW_ABI_VERSION = 1
-RTW_MAX_OPS = 4
+RTW_ABI_VERSION = 2
+RTW_MAX_OPS = 8
 
 # enums (rtw_gpu.h)
 RTW_PRIM_SPHERE, RTW_PRIM_MOVING_SPHERE, RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XZ, RTW_PRIM_RECT_YZ = range(5)
@@ -35,6 +35,7 @@ class rtw_prim(C.Structure):
 class rtw_entry(C.Structure):
     _fields_ = [("kind", C.c_int32), ("first_prim", C.c_int32), ("n_prims", C.c_int32), ("n_ops", C.c_int32),
                 ("op", C.c_int32 * RTW_MAX_OPS), ("phase_material", C.c_int32), ("bvh_root", C.c_int32),
+                ("n_outer_ops", C.c_int32), ("pad", C.c_int32),
                 ("op_param", (C.c_double * 3) * RTW_MAX_OPS), ("density", C.c_double), ("bounds", C.c_double * 6)]
 
 
@@ -72,7 +73,8 @@ class rtw_scene_desc(C.Structure):
                 ("materials", C.POINTER(rtw_material)), ("textures", C.POINTER(rtw_texture)),
                 ("lights", C.POINTER(rtw_light)), ("bvh_nodes", C.POINTER(rtw_bvh_node)),
                 ("bvh_items", C.POINTER(C.c_int32)), ("perlin_ranvec", C.POINTER(C.c_double)),
-                ("perlin_perm", C.POINTER(C.c_int32)), ("camera", rtw_camera_desc)]
+                ("perlin_perm", C.POINTER(C.c_int32)), ("camera", rtw_camera_desc),
+                ("visits", C.POINTER(C.c_int32)), ("n_visits", C.c_int32), ("pad", C.c_int32)]
 
 
 class rtw_render_params(C.Structure):

@@ -9,10 +9,25 @@
 // closest-so-far (hittable_list.h:15) picks the same winner, with the same
 // tie order, as the same primitives inlined at that position.
 //
+// Nesting of any depth: a list (or box, bvh_node, flip_normals, translate,
+// rotate_y) whose subtree holds transforms or media is taken apart -- its
+// children become entries of their own, in list order, each carrying the
+// op chain of every transform above it (the enclosing ops first).  A
+// deterministic subtree is inlined with one walk: hittable_list::hit walks
+// its objects twice (hittable_list.h:16-34), and for objects without random
+// draws the second walk re-accepts only what the first kept.  A list that
+// holds media is not: each medium draws again in the second walk.  Such
+// scenes get a visit program (rtw_scene_desc::visits): the entries in the
+// order the reference's nested walks call them, both walks of every list
+// that holds media, second-walk visits flagged RTW_VISIT_REPLAY (a
+// deterministic replay can only re-accept an exact tie; the GPU skips those,
+// the oracle runs them all).
+//
 // Light list members become rtw_light records with their own primitive copy
 // (entry = -1): hittable_pdf only ever queries them through their own
 // pdf_value/random overrides (pdf.h:35-53).
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -157,6 +172,8 @@ struct flattener {
     std::map<const texture*, int> tex_ids;
     bool perlin = false;
     std::string err;
+    bool nesting = false;  // collect() met a transform or medium
+    bool any_media = false;
     // the camera's shutter interval: rays carry times in [shutter0, shutter1]
     // (camera.h:41), so a moving sphere's BVH box must cover its centres over
     // that interval -- movement_linear extrapolates outside [time0, time1]
@@ -288,7 +305,7 @@ struct flattener {
                 if (!collect(o.get(), flip, entry)) return false;
             return true;
         }
-        err = "unsupported nesting: transforms / media must not appear inside a grouped list";
+        nesting = true;  // a transform or medium below: the caller takes the subtree apart
         return false;
     }
 
@@ -326,25 +343,16 @@ struct flattener {
         }
     }
 
-    bool add_entry(const hittable* h) {
-        rtw_entry e;
-        std::memset(&e, 0, sizeof e);
-        e.phase_material = -1;
-        e.bvh_root = -1;
-        e.kind = RTW_ENTRY_GROUP;
+    // One entry over `body` (a group of leaves, or a medium's boundary) with
+    // the ops `chain` (outermost first).
+    bool make_entry(rtw_entry e, const hittable* body) {
         const int id = (int)entries.size();
-        const hittable* body = h;
-        if (auto cm = dynamic_cast<const constant_medium*>(h)) {
-            e.kind = RTW_ENTRY_MEDIUM;
-            e.density = cm->density;
-            e.phase_material = material_id(cm->mp.get());
-            if (e.phase_material < 0) return false;
-            body = cm->boundary.get();
-        }
-        body = peel_ops(body, e);
-        if (!body) return false;
         e.first_prim = (int)prims.size();
-        if (!collect(body, 0, id)) return false;
+        nesting = false;
+        if (!collect(body, 0, id)) {
+            if (nesting && err.empty()) err = "a constant_medium boundary must not hold transforms or media";
+            return false;
+        }
         e.n_prims = (int)prims.size() - e.first_prim;
         if (e.n_prims == 0) {
             err = "empty group";
@@ -352,6 +360,105 @@ struct flattener {
         }
         entry_bounds(e);
         entries.push_back(e);
+        return true;
+    }
+
+    // Append `ops` to the chain of entry `e`.
+    bool push_ops(rtw_entry& e, const std::vector<std::pair<int, std::array<double, 3>>>& ops) {
+        for (const auto& o : ops) {
+            if (e.n_ops >= RTW_MAX_OPS) {
+                err = "more than RTW_MAX_OPS nested transforms";
+                return false;
+            }
+            e.op[e.n_ops] = o.first;
+            for (int a = 0; a < 3; ++a) e.op_param[e.n_ops][a] = o.second[a];
+            e.n_ops++;
+        }
+        return true;
+    }
+
+    using op_chain = std::vector<std::pair<int, std::array<double, 3>>>;
+
+    // Flatten one object of a list: entries for it (appended in list order)
+    // and the visits one call of its hit() makes (`out`).  `prefix`: the ops
+    // of the transforms enclosing it, outermost first.
+    bool flatten_node(const hittable* h, const op_chain& prefix, std::vector<int32_t>& out, bool& media) {
+        rtw_entry e;
+        std::memset(&e, 0, sizeof e);
+        e.phase_material = -1;
+        e.bvh_root = -1;
+        e.kind = RTW_ENTRY_GROUP;
+        if (!push_ops(e, prefix)) return false;
+        if (auto cm = dynamic_cast<const constant_medium*>(h)) {
+            e.kind = RTW_ENTRY_MEDIUM;
+            e.density = cm->density;
+            e.phase_material = material_id(cm->mp.get());
+            if (e.phase_material < 0) return false;
+            e.n_outer_ops = e.n_ops;  // the enclosing transforms; the boundary's own follow
+            const hittable* body = peel_ops(cm->boundary.get(), e);
+            if (!body) return false;
+            const int id = (int)entries.size();
+            if (!make_entry(e, body)) return false;
+            out.push_back(id);
+            media = true;
+            any_media = true;
+            return true;
+        }
+        const hittable* body = peel_ops(h, e);
+        if (!body) return false;
+        // a deterministic group of leaves: one entry
+        {
+            const size_t np = prims.size();
+            const int id = (int)entries.size();
+            nesting = false;
+            e.first_prim = (int)np;
+            if (collect(body, 0, id)) {
+                e.n_prims = (int)prims.size() - e.first_prim;
+                if (e.n_prims == 0) {
+                    err = "empty group";
+                    return false;
+                }
+                entry_bounds(e);
+                entries.push_back(e);
+                out.push_back(id);
+                return true;
+            }
+            if (!nesting || !err.empty()) return false;
+            prims.resize(np);  // take it apart instead
+        }
+        // the chain peeled so far becomes the children's prefix
+        op_chain inner;
+        for (int k = 0; k < e.n_ops; ++k)
+            inner.push_back({e.op[k], {e.op_param[k][0], e.op_param[k][1], e.op_param[k][2]}});
+        std::vector<const hittable*> kids;
+        if (auto f = dynamic_cast<const flip_normals*>(body)) {  // flip over a subtree with transforms
+            inner.push_back({RTW_OP_FLIP, {0, 0, 0}});
+            kids.push_back(f->ptr.get());
+        } else if (auto b = dynamic_cast<const box*>(body)) {
+            kids.push_back(&b->list_ptr);
+        } else if (auto l = dynamic_cast<const hittable_list*>(body)) {
+            for (const auto& o : l->objects) kids.push_back(o.get());
+        } else if (auto bn = dynamic_cast<const bvh_node*>(body)) {
+            for (const auto& o : bn->objects) kids.push_back(o.get());
+        } else {
+            err = "unsupported hittable in the scene graph";
+            return false;
+        }
+        const bool is_list = !dynamic_cast<const flip_normals*>(body);
+        std::vector<int32_t> seq;
+        bool m = false;
+        for (const hittable* k : kids) {
+            if (!k) {
+                err = "null object";
+                return false;
+            }
+            if (!flatten_node(k, inner, seq, m)) return false;
+        }
+        out.insert(out.end(), seq.begin(), seq.end());
+        if (m && is_list) {  // the list's second walk (hittable_list.h:26-34)
+            for (int32_t v : seq) out.push_back(v | RTW_VISIT_REPLAY);
+        }
+        media = media || m;
         return true;
     }
 
@@ -452,9 +559,18 @@ int rtw_flatten_world(const hittable_list& world, const hittable_list* lights, c
         f.shutter0 = std::min(cd.time0, cd.time1);
         f.shutter1 = std::max(cd.time0, cd.time1);
     }
+    // the world list, one call of its hit(): both walks when it holds media
+    std::vector<int32_t> visits;
     for (const auto& o : world.objects) {
-        if (!o || !f.add_entry(o.get()))
+        bool m = false;
+        if (!o || !f.flatten_node(o.get(), {}, visits, m))
             return rtw_fail(RTW_ERR_UNSUPPORTED, "rtw_flatten_scene: " + (f.err.empty() ? std::string("null object") : f.err));
+    }
+    if (f.any_media) {
+        const size_t n = visits.size();
+        for (size_t k = 0; k < n; ++k) visits.push_back(visits[k] | RTW_VISIT_REPLAY);
+    } else {
+        visits.clear();  // one walk over the entries is the reference's two
     }
     if (lights) {
         for (const auto& o : lights->objects)
@@ -528,6 +644,8 @@ int rtw_flatten_world(const hittable_list& world, const hittable_list* lights, c
     d->lights = rtw_dup(f.lights);
     d->bvh_nodes = rtw_dup(f.nodes);
     d->bvh_items = rtw_dup(f.items);
+    d->n_visits = (int)visits.size();
+    d->visits = visits.empty() ? nullptr : rtw_dup(visits);
     if (f.perlin) {
         std::vector<double> rv(perlin::SIZE * 3);
         std::vector<int32_t> pm(perlin::SIZE * 3);
@@ -556,6 +674,7 @@ extern "C" void rtw_scene_desc_free(rtw_scene_desc* d) {
     free((void*)d->bvh_items);
     free((void*)d->perlin_ranvec);
     free((void*)d->perlin_perm);
+    free((void*)d->visits);
     delete d;
 }
 

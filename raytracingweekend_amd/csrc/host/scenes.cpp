@@ -199,7 +199,72 @@ book2_final_scene::book2_final_scene(double aspect) {
     background_type = BackgroundType::Black;
 }
 
+// A test scene for arbitrary nesting (not in the reference; composed the
+// same way in oracle/ref_harness.cpp from the reference's classes): the
+// Cornell room, then instanced boxes inside a list, a flip over a list
+// holding a transformed rect, a medium inside a nested list, a medium inside
+// a translated list, and lists two deep under rotate_y / translate.
+nested_scene::nested_scene(double aspect) {
+    auto red = diffuse(0.65f, 0.05f, 0.05f);
+    auto white = diffuse(0.73f, 0.73f, 0.73f);
+    auto green = diffuse(0.12f, 0.45f, 0.15f);
+    auto light = std::make_shared<diffuse_light>(solid(15.0, 15.0, 15.0));
+    auto glass = std::make_shared<dielectric>(1.5);
+    using list = std::vector<std::shared_ptr<hittable>>;
+    auto L_ = [](list v) { return std::make_shared<hittable_list>(v); };
+
+    auto lamp = std::make_shared<xz_rect>(213.0, 343.0, 227.0, 332.0, 554.0, light);
+    Add(lamp);
+    lights->objects.push_back(lamp);
+    const double W = 555.0;
+    Add(std::make_shared<flip_normals>(std::make_shared<yz_rect>(0.0, W, 0.0, W, W, green)));
+    Add(std::make_shared<yz_rect>(0.0, W, 0.0, W, 0.0, red));
+    Add(std::make_shared<flip_normals>(std::make_shared<xz_rect>(0.0, W, 0.0, W, W, white)));
+    Add(std::make_shared<xz_rect>(0.0, W, 0.0, W, 0.0, white));
+    Add(std::make_shared<flip_normals>(std::make_shared<xy_rect>(0.0, W, 0.0, W, W, white)));
+    // instanced boxes in a list
+    Add(L_({std::make_shared<translate>(
+                std::make_shared<rotate_y>(std::make_shared<box>(vec3(0, 0, 0), vec3(80, 80, 80), white), 30.0),
+                vec3(60, 0, 350)),
+            std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(60, 120, 60), red),
+                                        vec3(420, 0, 380)),
+            std::make_shared<rotate_y>(
+                std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(50, 50, 50), green),
+                                            vec3(300, 0, 100)),
+                -10.0)}));
+    // a flip over a list holding a transformed rect
+    Add(std::make_shared<flip_normals>(
+        L_({std::make_shared<translate>(std::make_shared<xy_rect>(0.0, 100.0, 0.0, 100.0, 0.0, white),
+                                        vec3(230, 300, 500))})));
+    // a medium inside a nested list (a glass ball full of fog)
+    auto ball = std::make_shared<sphere>(vec3(150, 60, 150), 60.0, glass);
+    lights->objects.push_back(ball);
+    Add(L_({ball,
+            std::make_shared<constant_medium>(std::make_shared<sphere>(vec3(150, 60, 150), 55.0, glass), 0.02,
+                                              std::make_shared<isotropic>(solid(0.9, 0.9, 0.9))),
+            std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(40, 40, 40), white),
+                                        vec3(60, 0, 60))}));
+    // a medium inside a translated list
+    Add(std::make_shared<translate>(
+        L_({std::make_shared<constant_medium>(
+                std::make_shared<rotate_y>(std::make_shared<box>(vec3(0, 0, 0), vec3(100, 100, 100), white), 20.0),
+                0.01, std::make_shared<isotropic>(solid(0.2, 0.4, 0.9))),
+            std::make_shared<sphere>(vec3(50, 150, 50), 30.0,
+                                     std::make_shared<metal>(vec3(0.8, 0.85, 0.88), 0.1))}),
+        vec3(350, 0, 150)));
+    // lists two deep under transforms
+    Add(L_({L_({std::make_shared<translate>(std::make_shared<sphere>(vec3(0, 0, 0), 40.0, white),
+                                            vec3(400, 300, 300))}),
+            std::make_shared<rotate_y>(
+                L_({std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(50, 50, 50), red),
+                                                vec3(100, 350, 250))}),
+                20.0)}));
+    cam = look(vec3(278.0, 278.0, -800.0), vec3(278.0, 278.0, 0.0), 40.0, aspect, 0.0, 10.0);
+    background_type = BackgroundType::Black;
+}
+
 std::unique_ptr<scene> make_builtin_scene(const std::string& name, double aspect) {
+    if (name == "nested") return std::make_unique<nested_scene>(aspect);
     if (name == "cornell_box") return std::make_unique<cornell_box_scene>(aspect);
     if (name == "random_balls") return std::make_unique<random_balls_scene>(aspect);
     if (name == "dielectric") return std::make_unique<dielectric_scene>(aspect);

@@ -161,7 +161,7 @@ struct scene {
     int32_t n_entries, n_lights, world_bvh_root, render_type, background;
     int32_t has_media;
     int32_t n_media;
-    const int32_t* media;  // entry indices of media, in list order
+    const int32_t* media;  // the media walk: entry indices in visit order (upload_scene)
     // World list as runs (world_closest)
     const world_run* runs;
     const int32_t* entry_movers;  // per entry: its group holds DP_MOVING_COMMON* spheres
@@ -363,19 +363,34 @@ RTW_D void op_rec_out(const rtw_entry* E, int k, d3& p, d3& n) {
     }
 }
 
-// Statically indexed op chain (no runtime-indexed register arrays).
+// Ops [k0, k1) of an entry's chain on the way in, and [0, k1) on the way
+// out.  The first kOpsUnrolled are statically indexed (unrolled, each behind
+// its count test: a rolled loop over them measured 8 % slower on Cornell);
+// longer chains (nested transforms) continue in a loop.
+constexpr int kOpsUnrolled = 4;
 template <bool U>
-RTW_D ray entry_local_ray(const entry_v& e, ray r) {
+RTW_D ray ops_in(const entry_v& e, ray r, int k0, int k1) {
 #pragma unroll
-    for (int k = 0; k < RTW_MAX_OPS; ++k)
-        if (k < e.n_ops) op_ray_in<U>(e.p, k, r);
+    for (int k = 0; k < kOpsUnrolled; ++k)
+        if (k >= k0 && k < k1) op_ray_in<U>(e.p, k, r);
+    for (int k = kOpsUnrolled; k < k1; ++k)
+        if (k >= k0) op_ray_in<U>(e.p, k, r);
     return r;
 }
 template <bool U>
-RTW_D void entry_rec_out(const entry_v& e, d3& p, d3& n) {
+RTW_D void ops_out(const entry_v& e, int k1, d3& p, d3& n) {
+    for (int k = k1 - 1; k >= kOpsUnrolled; --k) op_rec_out<U>(e.p, k, p, n);
 #pragma unroll
-    for (int k = RTW_MAX_OPS - 1; k >= 0; --k)
-        if (k < e.n_ops) op_rec_out<U>(e.p, k, p, n);
+    for (int k = kOpsUnrolled - 1; k >= 0; --k)
+        if (k < k1) op_rec_out<U>(e.p, k, p, n);
+}
+template <bool U>
+RTW_D ray entry_local_ray(const entry_v& e, ray r) {
+    return ops_in<U>(e, r, 0, e.n_ops);
+}
+template <bool U>
+RTW_D void entry_rec_out(const entry_v& e, d3& p, d3& n) {
+    ops_out<U>(e, e.n_ops, p, n);
 }
 
 // ------------------------------------------------------------------ traversal
@@ -800,10 +815,11 @@ RTW_D void group_closest(const scene& S, const entry_v& e, const ray& r, double 
 }
 
 // Closest t of a medium's boundary in (t0, t1) (hittable.h:438-449); the
-// boundary is the entry's ops + group.
+// boundary is the entry's ops after the enclosing ones + group, `r` the ray
+// in the medium's frame.
 template <int F, class STK>
 RTW_D bool boundary_t(const scene& S, const entry_v& e, const ray& r, double t0, double t1, double& t, STK& stk) {
-    const ray lr = entry_local_ray<true>(e, r);
+    const ray lr = ops_in<true>(e, r, rd<true>(&e.p->n_outer_ops), e.n_ops);
     hit_state h{t1, -1, false};
     group_closest<F>(S, e, lr, t0, h, stk);
     if (h.prim == -1) return false;
@@ -811,10 +827,13 @@ RTW_D bool boundary_t(const scene& S, const entry_v& e, const ray& r, double t0,
     return true;
 }
 
-// constant_medium::hit hittable.h:430-479 (at most one draw per call)
+// constant_medium::hit hittable.h:430-479 (at most one draw per call), in
+// the frame of the transforms enclosing the medium (translate / rotate_y
+// hand it their moved ray, hittable.h:299-311, 373-404)
 template <int F, class STK>
-RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& r, double t_min, double t_max, uint32_t& rng,
+RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_min, double t_max, uint32_t& rng,
                     double& t_out, STK& stk) {
+    const ray r = ops_in<true>(e, rw, 0, rd<true>(&e.p->n_outer_ops));
     double t1, t2;
     if (!boundary_t<F>(S, e, r, -kDblMax, kDblMax, t1, stk)) return false;
     if (!boundary_t<F>(S, e, r, t1 + kStep, kDblMax, t2, stk)) return false;
@@ -909,9 +928,11 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
         return h;
     } else {
         if constexpr ((F & F_MEDIA) != 0) {
-            // entry by entry: with media the run form spills more registers
-            // than it saves (measured, Book-2 BVH)
-            for (int ei = 0; ei < S.n_entries; ++ei) {
+            // the media walk: entries in the order the reference's nested
+            // list walks call them (scene::media; with media the run form
+            // spills more registers than it saves, measured on Book-2 BVH)
+            for (int k = 0; k < S.n_media; ++k) {
+                const int ei = ld(&S.media[k]);
                 const entry_v e = view_entry<true>(S.entries, S.entry_movers, ei);
                 if (e.kind == RTW_ENTRY_MEDIUM) {
                     double t;
@@ -947,18 +968,6 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                                                       kTMin, h, ld(&S.runs[ri].movers));
             }
         }
-        if (F & F_MEDIA) {
-            for (int k = 0; k < S.n_media; ++k) {
-                const int ei = ld(&S.media[k]);
-                const entry_v e = view_entry<true>(S.entries, S.entry_movers, ei);
-                double t;
-                if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk)) {
-                    h.t = t;
-                    h.prim = -(2 + ei);
-                    h.rect = false;
-                }
-            }
-        }
         return h;
     }
 }
@@ -975,9 +984,13 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng) {
 template <bool MEDIA = true, bool STATIC = false>
 RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d3& n, int& mat, bool& rect) {
     rect = false;
-    if (MEDIA && h.prim <= -2) {  // constant_medium, hittable.h:469-472
-        p = at(r, h.t);
+    if (MEDIA && h.prim <= -2) {  // constant_medium, hittable.h:469-472, then its enclosing ops outward
+        const entry_v e = view_entry<false>(S.entries, S.entry_movers, -h.prim - 2);
+        const int n_outer = e.p->n_outer_ops;
+        const ray mr = ops_in<false>(e, r, 0, n_outer);
+        p = at(mr, h.t);
         n = d3{1, 0, 0};
+        ops_out<false>(e, n_outer, p, n);
         mat = S.entries[-h.prim - 2].phase_material;
         return;
     }

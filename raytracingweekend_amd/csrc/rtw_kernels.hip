@@ -1287,9 +1287,26 @@ size_t fresh_bytes(uint32_t cap) { return (size_t)cap * (7 * 8 + 2 * 4); }
 
 int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     // one allocation, 256-byte aligned sub-arrays
+    // The media walk (scene::media, world_closest with F_MEDIA): the visit
+    // program (rtw_scene_desc::visits) without its deterministic replays --
+    // a second walk over an object with no random draws re-accepts only an
+    // exact tie -- or, without a program, the world's two walks the same way:
+    // every entry, then the media again.
     std::vector<int32_t> media;
-    for (int e = 0; e < d->n_entries; ++e)
-        if (d->entries[e].kind == RTW_ENTRY_MEDIUM) media.push_back(e);
+    bool has_media = false;
+    for (int e = 0; e < d->n_entries; ++e) has_media |= d->entries[e].kind == RTW_ENTRY_MEDIUM;
+    if (has_media) {
+        if (d->n_visits > 0) {
+            for (int k = 0; k < d->n_visits; ++k) {
+                const int e = d->visits[k] & RTW_VISIT_ENTRY;
+                if (!(d->visits[k] & RTW_VISIT_REPLAY) || d->entries[e].kind == RTW_ENTRY_MEDIUM) media.push_back(e);
+            }
+        } else {
+            for (int e = 0; e < d->n_entries; ++e) media.push_back(e);
+            for (int e = 0; e < d->n_entries; ++e)
+                if (d->entries[e].kind == RTW_ENTRY_MEDIUM) media.push_back(e);
+        }
+    }
     struct part {
         const void* src;
         size_t bytes;
@@ -1565,8 +1582,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.render_type = d->render_type;
     S.background = d->background;
     S.n_media = (int32_t)media.size();
-    S.has_media = media.empty() ? 0 : 1;
-    h->media = !media.empty();
+    S.has_media = has_media ? 1 : 0;
+    h->media = has_media;
     h->features = (h->media ? F_MEDIA : 0) | (bvh_ok && d->world_bvh_root >= 0 ? F_WBVH : 0);
     h->ysph = false;
     for (const world_run& R : runs) h->ysph = h->ysph || R.entry == WORLD_RUN_YSPHERES;
@@ -1851,6 +1868,8 @@ int validate_desc(const rtw_scene_desc* d) {
         if (E.first_prim < 0 || E.n_prims <= 0 || E.first_prim + E.n_prims > d->n_prims)
             return rtw_fail(RTW_ERR_INVALID, "entry " + std::to_string(e) + ": prim range out of bounds");
         if (E.n_ops < 0 || E.n_ops > RTW_MAX_OPS) return rtw_fail(RTW_ERR_INVALID, "entry op count out of range");
+        if (E.n_outer_ops < 0 || E.n_outer_ops > E.n_ops || (E.kind != RTW_ENTRY_MEDIUM && E.n_outer_ops != 0))
+            return rtw_fail(RTW_ERR_INVALID, "entry outer op count out of range");
         if (E.kind == RTW_ENTRY_MEDIUM && (E.phase_material < 0 || E.phase_material >= d->n_materials))
             return rtw_fail(RTW_ERR_INVALID, "medium phase material out of range");
         if (E.bvh_root >= d->n_bvh_nodes) return rtw_fail(RTW_ERR_INVALID, "entry bvh root out of range");
@@ -1901,6 +1920,14 @@ int validate_desc(const rtw_scene_desc* d) {
         if (L.kind != RTW_LIGHT_DEFAULT && (L.prim < 0 || L.prim >= d->n_prims))
             return rtw_fail(RTW_ERR_INVALID, "light prim out of range");
     }
+    if (d->n_visits < 0 || (d->n_visits > 0 && !d->visits)) return rtw_fail(RTW_ERR_INVALID, "bad visit program");
+    for (int k = 0; k < d->n_visits; ++k) {
+        const int v = d->visits[k];
+        if (v < 0 || (v & ~(RTW_VISIT_ENTRY | RTW_VISIT_REPLAY)) || (v & RTW_VISIT_ENTRY) >= d->n_entries)
+            return rtw_fail(RTW_ERR_INVALID, "visit " + std::to_string(k) + " out of range");
+    }
+    if (d->n_visits > 0 && d->world_bvh_root >= 0)
+        return rtw_fail(RTW_ERR_UNSUPPORTED, "a visit program walks the list: no world BVH with it");
     if (d->world_bvh_root >= d->n_bvh_nodes) return rtw_fail(RTW_ERR_INVALID, "world bvh root out of range");
     for (int k = 0; k < d->n_bvh_nodes; ++k) {
         const rtw_bvh_node& N = d->bvh_nodes[k];

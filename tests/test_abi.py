@@ -55,7 +55,7 @@ def test_struct_layouts_match_c(tmp_path):
         for f, _ in cls._fields_:
             assert int(out[f"{s}.{f}"]) == getattr(cls, f).offset, f"{s}.{f}"
     # sizes documented in the header
-    assert C.sizeof(_abi.rtw_prim) == 96 and C.sizeof(_abi.rtw_entry) == 192
+    assert C.sizeof(_abi.rtw_prim) == 96 and C.sizeof(_abi.rtw_entry) == 312
     assert C.sizeof(_abi.rtw_bvh_node) == 64 and C.sizeof(_abi.rtw_material) == 48
 
 

@@ -26,6 +26,9 @@ CASES = [
     ("light_sample", 48, 24, 4, 50, False),
     ("book2_final", 24, 24, 2, 50, False),
     ("book2_final", 24, 24, 2, 50, True),
+    # transforms and media inside nested lists (visit program, media frames)
+    ("nested", 48, 36, 4, 50, False),
+    ("nested", 40, 40, 3, 20, True),
 ]
 
 
@@ -135,7 +138,8 @@ def test_reference_default_config_matches_committed_render(gpu):
     assert rms < 2.5, rms
 
 
-@pytest.mark.parametrize("scene,bvh", [("cornell_box", False), ("random_balls", True), ("dielectric", False)])
+@pytest.mark.parametrize("scene,bvh", [("cornell_box", False), ("random_balls", True), ("dielectric", False),
+                                       ("nested", False)])
 def test_execution_forms_agree(gpu, monkeypatch, scene, bvh):
     """The persistent kernel with material regrouping (k_persist_sort) and
     without it (k_persist) -- RTW_SORT=1/0, read once per process, so run in

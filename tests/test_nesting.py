@@ -1,0 +1,173 @@
+"""Arbitrary nesting: the flattener against an independent model of its
+rules, walked over the reference's own dump of the nested test scene
+(tests/golden/scene_nested.json, from oracle/_ref/rtw_ref; the scene is
+composed in oracle/ref_harness.cpp and, with this library's host API, in
+raytracingweekend_amd/csrc/host/scenes.cpp).
+
+Rules (raytracingweekend_amd/csrc/host/flatten.cpp): a subtree of leaves,
+flips, boxes and lists is one entry; a subtree holding transforms or media is
+taken apart, its children becoming entries in list order under the op chain
+of every transform above them (a flip over such a subtree becomes a FLIP op);
+a list holding media is visited twice (hittable_list.h:16-34), the second
+walk flagged RTW_VISIT_REPLAY; the world likewise.  The renders of this
+scene by the reference and by the C restatement are compared bit for bit in
+tests/test_oracle.py (renders.json); the GPU in tests/test_gpu_parity.py.
+"""
+import ctypes as C
+import json
+from pathlib import Path
+
+import pytest
+
+from raytracingweekend_amd import _abi
+from raytracingweekend_amd.render import SceneDesc
+
+GOLD = Path(__file__).resolve().parent / "golden"
+RECT = {"xy_rect": _abi.RTW_PRIM_RECT_XY, "xz_rect": _abi.RTW_PRIM_RECT_XZ, "yz_rect": _abi.RTW_PRIM_RECT_YZ}
+REPLAY, ENTRY = 0x40000000, 0x3FFFFFFF
+
+
+def _collectable(n):
+    t = n["type"]
+    if t in RECT or t in ("sphere", "moving_sphere"):
+        return True
+    if t == "flip":
+        return _collectable(n["ptr"])
+    if t == "box":
+        return _collectable(n["list"])
+    if t == "list":
+        return all(_collectable(o) for o in n["objects"])
+    return False
+
+
+def _leaves(n, flip, out):
+    t = n["type"]
+    if t in RECT:
+        out.append((RECT[t], tuple(n["p"]), flip))
+    elif t == "sphere":
+        out.append((_abi.RTW_PRIM_SPHERE, tuple(n["center"]) + (n["radius"],), flip))
+    elif t == "flip":
+        _leaves(n["ptr"], flip + 1, out)
+    elif t == "box":
+        _leaves(n["list"], flip, out)
+    elif t == "list":
+        for o in n["objects"]:
+            _leaves(o, flip, out)
+    else:
+        raise AssertionError(t)
+
+
+def _peel(n, ops):
+    while True:
+        t = n["type"]
+        if t == "translate":
+            ops.append((_abi.RTW_OP_TRANSLATE, tuple(n["offset"])))
+        elif t == "rotate_y":
+            ops.append((_abi.RTW_OP_ROTATE_Y, (n["sin"], n["cos"], 0.0)))
+        elif t == "flip" and n["ptr"]["type"] in ("translate", "rotate_y"):
+            ops.append((_abi.RTW_OP_FLIP, (0.0, 0.0, 0.0)))
+        else:
+            return n
+        n = n["ptr"]
+
+
+def model(world):
+    entries = []
+
+    def node(n, prefix):
+        """(visits of one hit() call, holds media)"""
+        if n["type"] == "constant_medium":
+            ops = list(prefix)
+            body = _peel(n["boundary"], ops)
+            prims = []
+            _leaves(body, 0, prims)
+            entries.append(("medium", len(prefix), ops, prims))
+            return [len(entries) - 1], True
+        ops = list(prefix)
+        body = _peel(n, ops)
+        if _collectable(body):
+            prims = []
+            _leaves(body, 0, prims)
+            entries.append(("group", 0, ops, prims))
+            return [len(entries) - 1], False
+        if body["type"] == "flip":
+            kids, inner, is_list = [body["ptr"]], ops + [(_abi.RTW_OP_FLIP, (0.0, 0.0, 0.0))], False
+        elif body["type"] == "box":
+            kids, inner, is_list = [body["list"]], ops, True
+        else:
+            assert body["type"] == "list", body["type"]
+            kids, inner, is_list = body["objects"], ops, True
+        seq, media = [], False
+        for k in kids:
+            v, m = node(k, inner)
+            seq += v
+            media = media or m
+        if media and is_list:
+            seq = seq + [v | REPLAY for v in seq]
+        return seq, media
+
+    visits, media = [], False
+    for o in world["objects"]:
+        v, m = node(o, [])
+        visits += v
+        media = media or m
+    visits = visits + [v | REPLAY for v in visits] if media else []
+    return entries, visits
+
+
+def test_nested_scene_flattens_as_modelled():
+    dump = json.loads((GOLD / "scene_nested.json").read_text())
+    want_entries, want_visits = model(dump["world"])
+    sd = SceneDesc("nested", dump["aspect"])
+    d = sd.desc
+    assert d.n_entries == len(want_entries)
+    assert [d.visits[k] for k in range(d.n_visits)] == want_visits
+    for i, (kind, n_outer, ops, prims) in enumerate(want_entries):
+        e = d.entries[i]
+        assert e.kind == (_abi.RTW_ENTRY_MEDIUM if kind == "medium" else _abi.RTW_ENTRY_GROUP), i
+        assert e.n_outer_ops == n_outer, i
+        assert e.n_ops == len(ops), i
+        for k, (op, prm) in enumerate(ops):
+            assert e.op[k] == op, (i, k)
+            assert tuple(e.op_param[k][a] for a in range(3)) == prm, (i, k)
+        assert e.n_prims == len(prims), i
+        for j, (ty, p, flip) in enumerate(prims):
+            q = d.prims[e.first_prim + j]
+            assert q.type == ty and q.flip == flip and q.entry == i, (i, j)
+            assert tuple(q.p[a] for a in range(len(p))) == p, (i, j)
+
+
+def test_media_entries_keep_their_enclosing_frame():
+    """The medium inside `translate(list(...))` measures its distances in the
+    translated frame: its chain starts with the enclosing translate, marked as
+    outer, then the boundary's own rotate_y."""
+    d = SceneDesc("nested", 1.0).desc
+    media = [d.entries[i] for i in range(d.n_entries) if d.entries[i].kind == _abi.RTW_ENTRY_MEDIUM]
+    assert [(m.n_outer_ops, m.n_ops) for m in media] == [(0, 0), (1, 2)]
+    assert media[1].op[0] == _abi.RTW_OP_TRANSLATE and media[1].op[1] == _abi.RTW_OP_ROTATE_Y
+
+
+@pytest.mark.parametrize("bad", ["visit", "outer"])
+def test_upload_rejects_bad_nesting_fields(bad):
+    """validate_desc checks the visit program and the outer-op counts
+    (no GPU needed: validation fails before any device call)."""
+    from raytracingweekend_amd._abi import lib
+    sd = SceneDesc("nested", 1.0)
+    d = sd.desc
+    if bad == "visit":
+        keep = d.visits[3]
+        d.visits[3] = d.n_entries + 5
+    else:
+        keep = d.entries[0].n_outer_ops
+        d.entries[0].n_outer_ops = 1
+    h = C.c_void_p()
+    try:
+        rc = lib().rtw_scene_upload(0, C.byref(d), C.byref(h))
+        assert rc != 0
+        msg = lib().rtw_last_error().decode()
+        assert ("visit" in msg) if bad == "visit" else ("outer op" in msg), msg
+    finally:
+        if bad == "visit":
+            d.visits[3] = keep
+        else:
+            d.entries[0].n_outer_ops = keep
