@@ -270,6 +270,8 @@ def main():
         value = samples_per_step * args.steps / elapsed / 1e6
         roof = roofline(args, info["kernel"], info["build_id"], seg, ms_isect, launches, algo) \
             if collect and ms_isect > 0 else None
+        if roof:
+            roof["bvh_lds_nodes"] = info["bvh_lds_nodes"]  # BVH node packet staged in LDS per workgroup
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),

@@ -40,7 +40,9 @@ extern "C" {
 #endif
 
 #define RTW_ABI_VERSION 2
+#ifndef RTW_MAX_OPS
 #define RTW_MAX_OPS 8
+#endif
 
 /* ------------------------------------------------------------------ */
 /* status codes                                                        */

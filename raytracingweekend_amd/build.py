@@ -91,13 +91,15 @@ def build_library(force: bool = False) -> Path:
     return LIB
 
 
-def build_variant_library(name: str, defines, force: bool = False) -> Path:
+def build_variant_library(name: str, defines, force: bool = False, host: bool = False) -> Path:
     """_build/librtw_<name>.so: the library with extra -D flags on the kernels
-    (tuning experiments; select with RTW_LIBRARY=...)."""
+    (and, host=True, on the host sources too: defines that change shared
+    layouts); tuning experiments, select with RTW_LIBRARY=..."""
     BUILD.mkdir(exist_ok=True)
     out = BUILD / f"librtw_{name}.so"
-    objs = [_compile(s, force, [f"-D{d}" for d in defines], f".{name}") for s in DEVICE_SOURCES]
-    objs += [_compile(s, force) for s in HOST_SOURCES]
+    flags = [f"-D{d}" for d in defines]
+    objs = [_compile(s, force, flags, f".{name}") for s in DEVICE_SOURCES]
+    objs += [_compile(s, force, flags, f".{name}") if host else _compile(s, force) for s in HOST_SOURCES]
     if force or _newer(out, objs):
         _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), *LIBS, "-o", str(out)])
     return out

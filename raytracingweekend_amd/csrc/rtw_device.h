@@ -145,9 +145,27 @@ struct bvh_node32;
 struct world_run {
     int32_t entry, first_prim, n_prims, movers;  // movers: the prims hold DP_MOVING_COMMON*
 };
+// Device form of a world-list entry (rtw_entry, built by the upload): the
+// header alone, its transform ops in one pool (scene::ops) -- 48 B instead of
+// the ABI's 312, so a scene's entries stay small in the LDS shading prefix
+// whatever RTW_MAX_OPS is, and op chains have no length limit here.
+struct dev_entry {
+    int32_t kind, first_prim, n_prims, n_ops;
+    int32_t first_op;     // ops [first_op, first_op + n_ops) of scene::ops, outermost first
+    int32_t phase_material, bvh_root;
+    int32_t n_outer_ops;  // MEDIUM: ops enclosing the medium (rtw_entry::n_outer_ops)
+    int32_t movers;       // the group holds DP_MOVING_COMMON* spheres
+    int32_t pad;
+    double density;
+};
+struct dev_op {
+    int32_t type, pad;
+    double p[3];
+};
 struct scene {
     const rtw_prim* prims;
-    const rtw_entry* entries;
+    const dev_entry* entries;
+    const dev_op* ops;
     const rtw_material* materials;
     const rtw_texture* textures;
     const rtw_light* lights;
@@ -164,7 +182,6 @@ struct scene {
     const int32_t* media;  // the media walk: entry indices in visit order (upload_scene)
     // World list as runs (world_closest)
     const world_run* runs;
-    const int32_t* entry_movers;  // per entry: its group holds DP_MOVING_COMMON* spheres
     int32_t n_runs;
     int32_t mv_common;     // some prims are DP_MOVING_COMMON*
     double mv_t0, mv_den;  // their time0 and time1 - time0
@@ -175,6 +192,13 @@ struct scene {
     // and r^2 of the filtered spheres
     const float* ysph;
     float ysb_cx, ysb_cy, ysb_dy, ysb_cz, ysb_r2;
+    // BVH node packets staged in LDS: the upload numbers the nodes of every
+    // BVH breadth-first from all roots together, so nodes [0, n_lnodes) are
+    // the top levels of every tree; the persistent BVH kernels copy them to
+    // LDS (lnodes) once per workgroup (n_lnodes = 0: all from memory)
+    const bvh_node32* lnodes;
+    int32_t n_lnodes;
+    int32_t n_nodes;  // device BVH nodes in all
 };
 
 // Scene features a traversal kernel is specialised for.
@@ -226,20 +250,23 @@ RTW_D T rd(const T* p) {
 // types and parameters (up to 4 ops x 3 doubles) read where an op is applied,
 // not all up front.
 struct entry_v {
-    const rtw_entry* p;
+    const dev_entry* p;
+    const dev_op* ops;  // its op chain
     int kind, first_prim, n_prims, n_ops, bvh_root;
-    bool movers;  // the group holds DP_MOVING_COMMON* spheres (scene::entry_movers)
+    bool movers;  // the group holds DP_MOVING_COMMON* spheres (dev_entry::movers)
 };
 template <bool U>
-RTW_D entry_v view_entry(const rtw_entry* E, const int32_t* M, int i) {
+RTW_D entry_v view_entry(const scene& S, int i) {
+    const dev_entry* E = S.entries;
     entry_v e;
     e.p = E + i;
+    e.ops = S.ops + rd<U>(&E[i].first_op);
     e.kind = rd<U>(&E[i].kind);
     e.first_prim = rd<U>(&E[i].first_prim);
     e.n_prims = rd<U>(&E[i].n_prims);
     e.n_ops = rd<U>(&E[i].n_ops);
     e.bvh_root = rd<U>(&E[i].bvh_root);
-    e.movers = rd<U>(&M[i]) != 0;
+    e.movers = rd<U>(&E[i].movers) != 0;
     return e;
 }
 
@@ -261,7 +288,7 @@ RTW_HD bool is_sphere(int type) { return type < RTW_PRIM_RECT_XY || type > RTW_P
 
 // The moving-sphere fraction (time - time0) / (time1 - time0) of the
 // scene's common interval, computed once per walk over prims that hold
-// DP_MOVING_COMMON* spheres (world_run::movers, scene::entry_movers; the
+// DP_MOVING_COMMON* spheres (world_run::movers, dev_entry::movers; the
 // walk's transforms keep the ray's time), else not at all.
 RTW_D double motion_frac(const scene& S, double time, bool movers) {
     return movers ? (time - S.mv_t0) / S.mv_den : 0.0;
@@ -332,12 +359,12 @@ RTW_HD d3 rect_normal(int type) {
 
 // translate::hit hittable.h:299-311, rotate_y::hit :373-404 (ray inward)
 template <bool U>
-RTW_D void op_ray_in(const rtw_entry* E, int k, ray& r) {
-    const int op = rd<U>(&E->op[k]);
+RTW_D void op_ray_in(const dev_op* O, int k, ray& r) {
+    const int op = rd<U>(&O[k].type);
     if (op == RTW_OP_TRANSLATE) {
-        r.o = r.o - d3{rd<U>(&E->op_param[k][0]), rd<U>(&E->op_param[k][1]), rd<U>(&E->op_param[k][2])};
+        r.o = r.o - d3{rd<U>(&O[k].p[0]), rd<U>(&O[k].p[1]), rd<U>(&O[k].p[2])};
     } else if (op == RTW_OP_ROTATE_Y) {
-        const double s = rd<U>(&E->op_param[k][0]), c = rd<U>(&E->op_param[k][1]);
+        const double s = rd<U>(&O[k].p[0]), c = rd<U>(&O[k].p[1]);
         const d3 o = r.o, d = r.d;
         r.o.x = c * o.x - s * o.z;
         r.o.z = s * o.x + c * o.z;
@@ -347,12 +374,12 @@ RTW_D void op_ray_in(const rtw_entry* E, int k, ray& r) {
 }
 // ... and the record outward (p, normal), innermost op first
 template <bool U>
-RTW_D void op_rec_out(const rtw_entry* E, int k, d3& p, d3& n) {
-    const int op = rd<U>(&E->op[k]);
+RTW_D void op_rec_out(const dev_op* O, int k, d3& p, d3& n) {
+    const int op = rd<U>(&O[k].type);
     if (op == RTW_OP_TRANSLATE) {
-        p = p + d3{rd<U>(&E->op_param[k][0]), rd<U>(&E->op_param[k][1]), rd<U>(&E->op_param[k][2])};
+        p = p + d3{rd<U>(&O[k].p[0]), rd<U>(&O[k].p[1]), rd<U>(&O[k].p[2])};
     } else if (op == RTW_OP_ROTATE_Y) {
-        const double s = rd<U>(&E->op_param[k][0]), c = rd<U>(&E->op_param[k][1]);
+        const double s = rd<U>(&O[k].p[0]), c = rd<U>(&O[k].p[1]);
         const d3 p0 = p, n0 = n;
         p.x = c * p0.x + s * p0.z;
         p.z = -s * p0.x + c * p0.z;
@@ -365,24 +392,26 @@ RTW_D void op_rec_out(const rtw_entry* E, int k, d3& p, d3& n) {
 
 // Ops [k0, k1) of an entry's chain on the way in, and [0, k1) on the way
 // out.  The first kOpsUnrolled are statically indexed (unrolled, each behind
-// its count test: a rolled loop over them measured 8 % slower on Cornell);
-// longer chains (nested transforms) continue in a loop.
-constexpr int kOpsUnrolled = 4;
+// its count test); longer chains (nested transforms) continue in a loop.
+#ifndef RTW_OPS_UNROLLED
+#define RTW_OPS_UNROLLED 4
+#endif
+constexpr int kOpsUnrolled = RTW_OPS_UNROLLED;
 template <bool U>
 RTW_D ray ops_in(const entry_v& e, ray r, int k0, int k1) {
 #pragma unroll
     for (int k = 0; k < kOpsUnrolled; ++k)
-        if (k >= k0 && k < k1) op_ray_in<U>(e.p, k, r);
+        if (k >= k0 && k < k1) op_ray_in<U>(e.ops, k, r);
     for (int k = kOpsUnrolled; k < k1; ++k)
-        if (k >= k0) op_ray_in<U>(e.p, k, r);
+        if (k >= k0) op_ray_in<U>(e.ops, k, r);
     return r;
 }
 template <bool U>
 RTW_D void ops_out(const entry_v& e, int k1, d3& p, d3& n) {
-    for (int k = k1 - 1; k >= kOpsUnrolled; --k) op_rec_out<U>(e.p, k, p, n);
+    for (int k = k1 - 1; k >= kOpsUnrolled; --k) op_rec_out<U>(e.ops, k, p, n);
 #pragma unroll
     for (int k = kOpsUnrolled - 1; k >= 0; --k)
-        if (k < k1) op_rec_out<U>(e.p, k, p, n);
+        if (k < k1) op_rec_out<U>(e.ops, k, p, n);
 }
 template <bool U>
 RTW_D ray entry_local_ray(const entry_v& e, ray r) {
@@ -741,11 +770,18 @@ struct local_stack {
     int s[kStack];
     RTW_D int& at(int i) { return s[i]; }
 };
-struct lds_stack {
+struct lds_stack {  // 16-bit node indices (LDS stacks need < 65536 nodes: upload)
     static constexpr int cap = kLdsStack;
-    int* p;  // &column[0][lane]; entry i at p[i * 256]
-    RTW_D int& at(int i) { return p[i * 256]; }
+    uint16_t* p;  // &column[0][lane]; entry i at p[i * 256]
+    RTW_D uint16_t& at(int i) { return p[i * 256]; }
 };
+
+// A BVH node: from the LDS packet when it is one of the top n_lnodes, else
+// from memory.
+RTW_D bvh_node32 node_at(const scene& S, int i) {
+    if (i < S.n_lnodes) return S.lnodes[i];
+    return S.nodes[i];
+}
 
 // Inner nodes carry their children's split axis (pad & 3) and whether the
 // left child lies on the upper side of it (pad & 4), set at upload: the
@@ -783,7 +819,7 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
     for (;;) {
         int la = 0, lc = 0;
         while (lc == 0 && sp > base) {
-            const bvh_node32 nd = S.nodes[stk.at(--sp)];
+            const bvh_node32 nd = node_at(S, stk.at(--sp));
             if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
             lc = node_count(nd);
             la = nd.a;
@@ -794,7 +830,7 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
     }
 #else
     while (sp > base) {
-        const bvh_node32 nd = S.nodes[stk.at(--sp)];
+        const bvh_node32 nd = node_at(S, stk.at(--sp));
         if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
         const int cnt = node_count(nd);
         if (cnt > 0) {
@@ -882,7 +918,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                         arbitrate(S, ~it, r, kTMin, h, fc);
                     continue;
                 }
-                const entry_v e = view_entry<false>(S.entries, S.entry_movers, it);
+                const entry_v e = view_entry<false>(S, it);
                 const ray lr = entry_local_ray<false>(e, r);
                 if ((F & F_GBVH) && e.bvh_root >= 0) {
                     group_bvh(S, e.bvh_root, lr, kTMin, h, stk, sp, S.mv_common != 0);
@@ -903,7 +939,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             for (;;) {
                 int la = 0, lc = 0;  // this lane's pending leaf: first item, count
                 while (lc == 0 && sp > 0) {
-                    const bvh_node32 nd = S.nodes[stk.at(--sp)];
+                    const bvh_node32 nd = node_at(S, stk.at(--sp));
                     if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
                     lc = node_count(nd);
                     la = nd.a;
@@ -915,7 +951,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             }
         } else {
             while (sp > 0) {
-                const bvh_node32 nd = S.nodes[stk.at(--sp)];
+                const bvh_node32 nd = node_at(S, stk.at(--sp));
                 if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
                 const int cnt = node_count(nd);
                 if (cnt > 0) {
@@ -933,7 +969,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             // spills more registers than it saves, measured on Book-2 BVH)
             for (int k = 0; k < S.n_media; ++k) {
                 const int ei = ld(&S.media[k]);
-                const entry_v e = view_entry<true>(S.entries, S.entry_movers, ei);
+                const entry_v e = view_entry<true>(S, ei);
                 if (e.kind == RTW_ENTRY_MEDIUM) {
                     double t;
                     if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk)) {
@@ -957,7 +993,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                 }
                 ray lr = r;
                 if (ei >= 0) {
-                    const entry_v e = view_entry<true>(S.entries, S.entry_movers, ei);
+                    const entry_v e = view_entry<true>(S, ei);
                     lr = entry_local_ray<true>(e, r);
                     if ((F & F_GBVH) && e.bvh_root >= 0) {
                         group_bvh(S, e.bvh_root, lr, kTMin, h, stk, 0, e.movers);
@@ -985,7 +1021,7 @@ template <bool MEDIA = true, bool STATIC = false>
 RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d3& n, int& mat, bool& rect) {
     rect = false;
     if (MEDIA && h.prim <= -2) {  // constant_medium, hittable.h:469-472, then its enclosing ops outward
-        const entry_v e = view_entry<false>(S.entries, S.entry_movers, -h.prim - 2);
+        const entry_v e = view_entry<false>(S, -h.prim - 2);
         const int n_outer = e.p->n_outer_ops;
         const ray mr = ops_in<false>(e, r, 0, n_outer);
         p = at(mr, h.t);
@@ -995,7 +1031,7 @@ RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d
         return;
     }
     const rtw_prim q = S.prims[h.prim];
-    const entry_v e = view_entry<false>(S.entries, S.entry_movers, q.entry);
+    const entry_v e = view_entry<false>(S, q.entry);
     const ray lr = entry_local_ray<false>(e, r);
     p = at(lr, h.t);
     if (is_sphere(q.type)) {

@@ -502,7 +502,8 @@ __device__ __forceinline__ scene lds_scene(const scene& S, const char* base, con
     scene L = S;
     auto rb = [&](const void* p) -> const void* { return p ? (const void*)(lds + ((const char*)p - base)) : nullptr; };
     L.prims = (const rtw_prim*)rb(S.prims);
-    L.entries = (const rtw_entry*)rb(S.entries);
+    L.entries = (const dev_entry*)rb(S.entries);
+    L.ops = (const dev_op*)rb(S.ops);
     L.materials = (const rtw_material*)rb(S.materials);
     L.textures = (const rtw_texture*)rb(S.textures);
     L.lights = (const rtw_light*)rb(S.lights);
@@ -636,6 +637,8 @@ struct persist_args {
     ctrs_t* C;
     const char* base;  // the scene allocation; its shading prefix is staged in LDS
     uint32_t bytes;    // bytes of that prefix
+    uint32_t lds_nodes;      // BVH node packet: the top nodes staged in LDS (k_persist, LST)
+    uint32_t lds_nodes_off;  // its byte offset in the dynamic LDS (after the prefix)
 };
 
 // The persistent kernels' argument, re-read from the kernarg segment (scalar
@@ -659,15 +662,22 @@ void k_persist(persist_args) {
     __shared__ uint32_t s_cnt[kWaves];
     __shared__ ray_batch s_batch[kWaves];
     __shared__ double s_thr[3][kBlock];  // each lane's path throughput
-    __shared__ int s_stack[LST ? kLdsStack : 1][kBlock];
+    __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kBlock];
     __shared__ uint32_t s_q[kBlock];     // each lane's sample id
     if (LDS) {
         const persist_args& A = args_now();
         const uint4* src = reinterpret_cast<const uint4*>(A.base);
         uint4* dst = reinterpret_cast<uint4*>(s_scene);
         for (uint32_t k = threadIdx.x; k < A.bytes / 16; k += kBlock) dst[k] = src[k];
-        __syncthreads();
     }
+    if (LST) {  // the BVH node packet (the top levels of every tree)
+        const persist_args& A = args_now();
+        const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
+        uint4* dst = reinterpret_cast<uint4*>(s_scene + A.lds_nodes_off);
+        for (uint32_t k = threadIdx.x; k < A.lds_nodes * (uint32_t)(sizeof(bvh_node32) / 16); k += kBlock)
+            dst[k] = src[k];
+    }
+    if (LDS || LST) __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     ray_batch& B = s_batch[threadIdx.x >> 6];
     const int own = blockIdx.x % kQShards;
@@ -740,9 +750,11 @@ void k_persist(persist_args) {
         pf.mark(PS_LOAD);
         if (x.depth != 0) {
             const persist_args& A = args_now();
-            const scene& S = A.S;
+            scene S = A.S;
             hit_state h;
             if constexpr (LST) {
+                S.lnodes = reinterpret_cast<const bvh_node32*>(s_scene + A.lds_nodes_off);
+                S.n_lnodes = (int32_t)A.lds_nodes;
                 lds_stack stk{&s_stack[0][threadIdx.x]};
                 h = world_closest<F>(S, x.r, x.rng, stk);
             } else {
@@ -1506,12 +1518,64 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         M.a = N.left;
         M.b = N.count > 0 ? -N.count : (N.right | (N.pad << 28));
     }
+    // Breadth-first numbering from all roots together (the world BVH's, then
+    // every group's, in entry order): nodes [0, k) are then the top levels of
+    // every tree, the node packet the persistent BVH kernels stage in LDS.
+    std::vector<rtw_entry> dentries(d->entries, d->entries + d->n_entries);
+    int world_root = d->world_bvh_root;
+    if (!dnodes32.empty()) {
+        std::vector<int> order, newid(dnodes32.size(), -1);
+        order.reserve(dnodes32.size());
+        auto enqueue = [&](int n) {
+            if (n >= 0 && newid[n] < 0) newid[n] = (int)order.size(), order.push_back(n);
+        };
+        enqueue(world_root);
+        for (const rtw_entry& E : dentries) enqueue(E.bvh_root);
+        for (size_t q = 0; q < order.size(); ++q) {
+            const rtw_bvh_node& N = dnodes[order[q]];
+            if (N.count == 0) enqueue(N.left), enqueue(N.right);
+        }
+        for (size_t n = 0; n < dnodes32.size(); ++n) enqueue((int)n);  // unreachable nodes keep a slot
+        std::vector<bvh_node32> bfs(dnodes32.size());
+        for (size_t n = 0; n < dnodes32.size(); ++n) {
+            bvh_node32 M = dnodes32[n];
+            if (M.b >= 0) {  // inner: renumber both children, keep the split bits
+                M.a = newid[M.a];
+                M.b = newid[M.b & 0x0fffffff] | (M.b & ~0x0fffffff);
+            }
+            bfs[newid[n]] = M;
+        }
+        dnodes32.swap(bfs);
+        if (world_root >= 0) world_root = newid[world_root];
+        for (rtw_entry& E : dentries)
+            if (E.bvh_root >= 0) E.bvh_root = newid[E.bvh_root];
+    }
+    // device entries (dev_entry) and their op pool
+    std::vector<dev_entry> dev_entries(std::max<size_t>(dentries.size(), 1));
+    std::vector<dev_op> dev_ops;
+    for (size_t e = 0; e < dentries.size(); ++e) {
+        const rtw_entry& E = dentries[e];
+        dev_entry& D = dev_entries[e];
+        std::memset(&D, 0, sizeof D);
+        D.kind = E.kind, D.first_prim = E.first_prim, D.n_prims = E.n_prims, D.n_ops = E.n_ops;
+        D.first_op = (int32_t)dev_ops.size();
+        D.phase_material = E.phase_material, D.bvh_root = E.bvh_root, D.n_outer_ops = E.n_outer_ops;
+        D.movers = entry_movers[e];
+        D.density = E.density;
+        for (int k = 0; k < E.n_ops; ++k) {
+            dev_op o;
+            std::memset(&o, 0, sizeof o);
+            o.type = E.op[k];
+            for (int j = 0; j < 3; ++j) o.p[j] = E.op_param[k][j];
+            dev_ops.push_back(o);
+        }
+    }
     std::vector<part> parts = {
-        // parts 0..9 are what shading reads; they come first so a small
+        // parts 0..10 are what shading reads; they come first so a small
         // scene's shading data is one contiguous prefix the shade kernel can
         // stage in LDS
         {dprims.data(), sizeof(rtw_prim) * dprims.size(), 0},
-        {d->entries, sizeof(rtw_entry) * d->n_entries, 0},
+        {dev_entries.data(), sizeof(dev_entry) * (size_t)d->n_entries, 0},
         {d->materials, sizeof(rtw_material) * d->n_materials, 0},
         {d->textures, sizeof(rtw_texture) * d->n_textures, 0},
         {d->lights, sizeof(rtw_light) * d->n_lights, 0},
@@ -1520,10 +1584,10 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {media.data(), sizeof(int32_t) * media.size(), 0},
         {frames.data(), sizeof(double) * frames.size(), 0},
         {mat_aux.data(), sizeof(double) * mat_aux.size(), 0},
+        {dev_ops.data(), sizeof(dev_op) * dev_ops.size(), 0},
         {dnodes32.data(), sizeof(bvh_node32) * dnodes32.size(), 0},
         {ditems.data(), sizeof(int32_t) * ditems.size(), 0},
         {runs.data(), sizeof(world_run) * runs.size(), 0},
-        {entry_movers.data(), sizeof(int32_t) * entry_movers.size(), 0},
         {ysph.data(), sizeof(float) * ysph.size(), 0},
     };
     size_t total = 0;
@@ -1541,7 +1605,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     auto at = [&](int k) { return parts[k].bytes ? (void*)(base + parts[k].off) : nullptr; };
     scene& S = h->S;
     S.prims = (const rtw_prim*)at(0);
-    S.entries = (const rtw_entry*)at(1);
+    S.entries = (const dev_entry*)at(1);
     S.materials = (const rtw_material*)at(2);
     S.textures = (const rtw_texture*)at(3);
     S.lights = (const rtw_light*)at(4);
@@ -1550,11 +1614,11 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.media = (const int32_t*)at(7);
     S.prim_onb = (const double*)at(8);
     S.mat_aux = (const double*)at(9);
-    S.nodes = (const bvh_node32*)at(10);
+    S.ops = (const dev_op*)at(10);
+    S.nodes = (const bvh_node32*)at(11);
     S.bvh_bound = bvh_bound;
-    S.items = (const int32_t*)at(11);
-    S.runs = (const world_run*)at(12);
-    S.entry_movers = (const int32_t*)at(13);
+    S.items = (const int32_t*)at(12);
+    S.runs = (const world_run*)at(13);
     S.ysph = (const float*)at(14);
     S.ysb_cx = ysb[0], S.ysb_cy = ysb[1], S.ysb_dy = ysb[2], S.ysb_cz = ysb[3], S.ysb_r2 = ysb[4];
     S.n_runs = (int32_t)runs.size();
@@ -1573,12 +1637,13 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         }
         S.fast_div = bounded ? 1 : 0;
     }
-    h->shade_bytes = (uint32_t)parts[10].off;  // the shading prefix
+    h->shade_bytes = (uint32_t)parts[11].off;  // the shading prefix
     h->scene_base = base;
     S.n_entries = d->n_entries;
     S.n_lights = d->n_lights;
     S.light_weight = d->n_lights > 0 ? 1.0 / (double)d->n_lights : 0.0;
-    S.world_bvh_root = bvh_ok ? d->world_bvh_root : -1;
+    S.world_bvh_root = bvh_ok ? world_root : -1;
+    S.n_nodes = (int32_t)dnodes32.size();
     S.render_type = d->render_type;
     S.background = d->background;
     S.n_media = (int32_t)media.size();
@@ -1730,9 +1795,40 @@ bool sort_forced(bool& value) {
     return true;
 }
 
+// BVH node packet of a k_persist<.., LST> launch: the most top nodes (BFS
+// numbering, rtw_scene_upload) that fit in LDS beside the kernel's own
+// arrays and the shading prefix without costing a workgroup per CU
+// (occupancy query per candidate size).  RTW_LDS_NODES=<n> caps it (0 = off:
+// A/B).  The node count of the last launch or probe is kept for
+// rtw_scene_query.
+thread_local uint32_t g_node_packet = 0;
+template <int FF, int MM, bool LL>
+uint32_t node_packet(size_t shm, int n_nodes) {
+    const char* e = std::getenv("RTW_LDS_NODES");
+    uint32_t cap = (e && *e) ? (uint32_t)std::max(0, std::atoi(e)) : 4096u;
+    cap = std::min<uint32_t>(cap, (uint32_t)std::max(0, n_nodes));
+    if (!cap) return 0;
+    const void* fn = reinterpret_cast<const void*>(&k_persist<FF, MM, LL, true>);
+    int base = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&base, fn, kBlock, shm) != hipSuccess || base <= 0) return 0;
+    const size_t off = (shm + 15) & ~size_t(15);
+    uint32_t best = 0;
+    for (uint32_t k = 32; k <= cap + 31; k += 32) {
+        const uint32_t kk = std::min(k, cap);
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kBlock, off + kk * sizeof(bvh_node32)) != hipSuccess ||
+            nb < base)
+            break;
+        best = kk;
+        if (kk == cap) break;
+    }
+    return best;
+}
+
 template <int FF, int MM, bool LL>
 void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t st, const scene& S, const job_t& J,
                ctrs_t* C, const char* base, uint32_t bytes, int stack_need) {
+    g_node_packet = 0;
     static const bool sorted = [] {
         bool v;
         return sort_forced(v) ? v : (FF & (F_WBVH | F_GBVH)) == 0;
@@ -1742,11 +1838,15 @@ void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t s
         if (!probe)
             hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)),
                                dim3(kSortBlock), shm, st, persist_args{S, J, C, base, bytes});
-    } else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack) {
+    } else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack && S.n_nodes < 65536) {  // 16-bit LDS stacks
         if (name) *name = kname("k_persist", FF, MM, LL, true);
+        const uint32_t packet = node_packet<FF, MM, LL>(shm, S.n_nodes);
+        const uint32_t off = (uint32_t)((shm + 15) & ~size_t(15));
+        g_node_packet = packet;
+        const size_t shm2 = packet ? off + packet * sizeof(bvh_node32) : shm;
         if (!probe)
             hipLaunchKernelGGL((k_persist<FF, MM, LL, true>), dim3(persist_grid<FF, MM, LL, true>(shm, cus)),
-                               dim3(kBlock), shm, st, persist_args{S, J, C, base, bytes});
+                               dim3(kBlock), shm2, st, persist_args{S, J, C, base, bytes, packet, off});
     } else {
         if (name) *name = kname("k_persist", FF, MM, LL, false);
         if (!probe)
@@ -2044,8 +2144,10 @@ extern "C" int rtw_scene_query(void* handle, rtw_scene_info* out) {
     out->features = h->features;
     out->shade_mask = h->shade_mask;
     out->shade_lds_bytes = h->shade_bytes <= kShadeLdsMax ? (int32_t)h->shade_bytes : 0;
-    out->bvh_lds_nodes = 0;
+    HIPCHK(hipSetDevice(h->device));  // occupancy queries of the probe
+    g_node_packet = 0;
     const std::string k = render_kernel_name(h);
+    out->bvh_lds_nodes = (int32_t)g_node_packet;  // set by the probe (launch_pk)
     std::snprintf(out->kernel, sizeof out->kernel, "%s", k.c_str());
     std::snprintf(out->build_id, sizeof out->build_id, "%s", RTW_BUILD_ID);
     return RTW_OK;

@@ -1,6 +1,8 @@
 #!/bin/bash
 # Instruction-mix / stall / HBM-byte counters of a short bench run, one
-# rocprofv3 --pmc pass per counter group (kernel-trace only).
+# rocprofv3 --pmc pass per counter group (kernel-trace only), folded into
+# profiles/pmc/<tag>.json (scripts/pmc_to_json.py: kernel, build and workload
+# taken from the measured bench lines).
 # Usage: scripts/pmc_passes.sh <tag> [bench args...]
 set -e
 tag=$1; shift
@@ -10,7 +12,10 @@ P3="SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INS
 P4="FETCH_SIZE GRBM_GUI_ACTIVE"
 P5="WRITE_SIZE GRBM_COUNT"
 i=1
+dirs=()
 for grp in "$P1" "$P2" "$P3" "$P4" "$P5"; do
     scripts/prof_pmc.sh "${tag}_$i" "$grp" "$@"
+    dirs+=("gpurun_out/pmc_${tag}_$i")
     i=$((i+1))
 done
+python3 scripts/pmc_to_json.py "gpurun_out/pmc/${tag}.json" "${dirs[@]}"

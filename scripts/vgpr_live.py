@@ -13,6 +13,9 @@ import re
 import sys
 from collections import defaultdict
 
+args = [a for a in sys.argv[1:] if a != "--sgpr"]
+SGPR = "--sgpr" in sys.argv  # analyse SGPRs instead (s_* defs, v_cmp/readlane/carry-out defs)
+sys.argv = [sys.argv[0]] + args
 path, fname = sys.argv[1], sys.argv[2]
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 12
 lines = open(path).read().splitlines()
@@ -28,7 +31,7 @@ start = next(i for i, l in enumerate(lines) if re.match(r"^\S*" + re.escape(fnam
              (fname in l and l.rstrip().endswith(":") and not l.startswith("\t")))
 end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))
 
-REG = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
+REG = re.compile(r"\bs(\d+)\b|\bs\[(\d+):(\d+)\]") if SGPR else re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
 NODEF = ("_store", "ds_write", "s_", "v_cmp_", "v_cmpx_", "v_readlane", "v_readfirstlane", "buffer_atomic",
          "global_atomic", "flat_atomic", "ds_add", "ds_max", "ds_min")
 
@@ -65,6 +68,27 @@ for i in range(start + 1, end):
     operands = [o.strip() for o in re.split(r",(?![^\[]*\])", ops)] if ops else []
     defs, uses = [], []
     glc_ret = op.endswith("_rtn") or " glc" in ops or "sc0" in ops
+    if SGPR:
+        if op.startswith(("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_waitcnt", "s_barrier", "s_nop",
+                          "s_endpgm", "s_setprio", "s_sleep", "s_store", "s_atomic", "s_dcache", "s_sendmsg")) or \
+                op.startswith(("v_", "ds_", "global_", "buffer_", "flat_", "scratch_")) and not (
+                op.startswith(("v_cmp_", "v_cmpx_", "v_readlane", "v_readfirstlane")) and "_e64" in op or
+                op.startswith(("v_readlane", "v_readfirstlane"))):
+            # no SGPR def in the first operand; carry-out / scale defs in the second
+            if op.startswith(("v_add_co", "v_sub_co", "v_subrev_co", "v_div_scale", "v_mad_u64", "v_mad_i64",
+                              "v_addc_co", "v_subb_co")) and len(operands) > 1:
+                defs += regs(operands[1])
+                for o in operands[:1] + operands[2:]:
+                    uses += regs(o)
+            else:
+                for o in operands:
+                    uses += regs(o)
+        elif operands:
+            defs += regs(operands[0])
+            for o in operands[1:]:
+                uses += regs(o)
+        insts.append((op, set(defs), set(uses), cur_loc, l))
+        continue
     if op.startswith(NODEF) and not (("atomic" in op) and glc_ret):
         for o in operands:
             uses += regs(o)
@@ -128,7 +152,7 @@ while changed:
             changed = True
 
 order = sorted(range(n), key=lambda k: -len(live_in[k]))
-print(f"{n} instructions; max live VGPRs {len(live_in[order[0]])}")
+print(f"{n} instructions; max live {'SGPRs' if SGPR else 'VGPRs'} {len(live_in[order[0]])}")
 seen_loc = set()
 shown = 0
 for k in order:
