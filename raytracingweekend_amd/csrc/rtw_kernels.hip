@@ -688,6 +688,13 @@ void k_persist(persist_args) {
     uint32_t segs = 0;
     prof_t pf;
     for (;;) {
+        // lane-dependent LDS addresses (batch, throughput, sample id, stack
+        // columns) are formed from an opaque copy of the thread index where
+        // they are used: left to itself the compiler hoists one VGPR per
+        // array out of the loop (C5's kernel: 65 of them)
+        uint32_t tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const uint32_t ln = tid & 63;
         for (int round = 0; round < 2; ++round) {
             const unsigned long long m = __ballot(x.depth == 0);
             if (!m) break;
@@ -703,7 +710,7 @@ void k_persist(persist_args) {
                     const int sh = (own + a) % kQShards;
                     const unsigned long long lim = shard_limit(sh, J.total);
                     unsigned long long b = ~0ull;
-                    if (lane == 0) {
+                    if (ln == 0) {
                         const bool dry = a > 0 && __hip_atomic_load(&C->qshard[sh].v, __ATOMIC_RELAXED,
                                                                     __HIP_MEMORY_SCOPE_AGENT) >= lim;
                         if (!dry) b = atomicAdd(&C->qshard[sh].v, (unsigned long long)left);
@@ -711,8 +718,8 @@ void k_persist(persist_args) {
                     b = __shfl(b, 0, 64);
                     if (b == ~0ull || b >= lim) continue;
                     const uint32_t ok = (uint32_t)min((unsigned long long)left, lim - b);
-                    if (lane >= given && lane < given + ok) {
-                        q = (uint32_t)shard_sample(sh, b + (lane - given));
+                    if (ln >= given && ln < given + ok) {
+                        q = (uint32_t)shard_sample(sh, b + (ln - given));
                         got = true;
                     }
                     given += ok;
@@ -722,11 +729,11 @@ void k_persist(persist_args) {
                 if (got) {
                     uint32_t rng;
                     const ray r = camera_sample(J, q, rng);
-                    B.ox[lane] = r.o.x, B.oy[lane] = r.o.y, B.oz[lane] = r.o.z;
-                    B.dx[lane] = r.d.x, B.dy[lane] = r.d.y, B.dz[lane] = r.d.z;
-                    B.tm[lane] = r.t;
-                    B.rng[lane] = rng;
-                    B.q[lane] = q;
+                    B.ox[ln] = r.o.x, B.oy[ln] = r.o.y, B.oz[ln] = r.o.z;
+                    B.dx[ln] = r.d.x, B.dy[ln] = r.d.y, B.dz[ln] = r.d.z;
+                    B.tm[ln] = r.t;
+                    B.rng[ln] = rng;
+                    B.q[ln] = q;
                 }
                 bl = 0;
                 bh = given;
@@ -739,8 +746,8 @@ void k_persist(persist_args) {
                 const uint32_t k = bl + rank;
                 x.r = ray{d3{B.ox[k], B.oy[k], B.oz[k]}, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
                 x.rng = B.rng[k];
-                s_q[threadIdx.x] = B.q[k];
-                s_thr[0][threadIdx.x] = 1.0, s_thr[1][threadIdx.x] = 1.0, s_thr[2][threadIdx.x] = 1.0;
+                s_q[tid] = B.q[k];
+                s_thr[0][tid] = 1.0, s_thr[1][tid] = 1.0, s_thr[2][tid] = 1.0;
                 x.depth = (uint32_t)args_now().J.max_depth;
             }
             bl += min((uint32_t)__popcll(m), avail);
@@ -755,7 +762,7 @@ void k_persist(persist_args) {
             if constexpr (LST) {
                 S.lnodes = reinterpret_cast<const bvh_node32*>(s_scene + A.lds_nodes_off);
                 S.n_lnodes = (int32_t)A.lds_nodes;
-                lds_stack stk{&s_stack[0][threadIdx.x]};
+                lds_stack stk{&s_stack[0][tid]};
                 h = world_closest<F>(S, x.r, x.rng, stk);
             } else {
                 h = world_closest<F>(S, x.r, x.rng);
@@ -770,7 +777,7 @@ void k_persist(persist_args) {
                                                         : SS.prims[h.prim].material].type);
 #endif
             // the outcome is applied inside the branch that produced it
-            const uint32_t me = threadIdx.x;
+            const uint32_t me = tid;
             auto radiance = [&](const d3& L) {
                 double* o = A2.J.L + 3 * (size_t)s_q[me];
                 o[0] = L.x, o[1] = L.y, o[2] = L.z;
