@@ -28,7 +28,7 @@ REF = ROOT / "oracle" / "_ref" / "rtw_ref"
 OUT = ROOT / "tests" / "golden"
 
 SCENES = [("cornell_box", 1.0), ("random_balls", 1.5), ("dielectric", 2.0), ("light_sample", 2.0),
-          ("book2_final", 1.0), ("nested", 1.0)]
+          ("book2_final", 1.0), ("nested", 1.0), ("nested_plain", 1.0)]
 
 # (case, scene, nx, ny, spp, depth, seed)
 RENDERS = [
@@ -42,6 +42,7 @@ RENDERS = [
     ("book2_final_16x16x2_d50", "book2_final", 16, 16, 2, 50, 0),
     ("nested_24x24x4_d50", "nested", 24, 24, 4, 50, 0),
     ("nested_32x24x3_d20", "nested", 32, 24, 3, 20, 3),
+    ("nested_plain_24x24x4_d50", "nested_plain", 24, 24, 4, 50, 1),
 ]
 
 # whole-image P3 files (case, scene, nx, ny, spp, depth, seed)

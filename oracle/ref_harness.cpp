@@ -148,7 +148,7 @@ public:
 // ---------------------------------------------------------------------------
 class nested_scene : public scene {
 public:
-    nested_scene(double aspect) : scene() {
+    nested_scene(double aspect, bool media = true) : scene() {
         auto solid = [](double r, double g, double b) { return std::make_shared<constant_texture>(vec3(r, g, b)); };
         auto red = std::make_shared<lambertian>(solid(0.65f, 0.05f, 0.05f));
         auto white = std::make_shared<lambertian>(solid(0.73f, 0.73f, 0.73f));
@@ -181,11 +181,16 @@ public:
                                             vec3(230, 300, 500))})));
         auto ball = std::make_shared<sphere>(vec3(150, 60, 150), 60.0, glass);
         lights->objects.push_back(ball);
-        Add(L_({ball,
-                std::make_shared<constant_medium>(std::make_shared<sphere>(vec3(150, 60, 150), 55.0, glass), 0.02,
-                                                  std::make_shared<isotropic>(solid(0.9, 0.9, 0.9))),
-                std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(40, 40, 40), white),
-                                            vec3(60, 0, 60))}));
+        if (media)
+            Add(L_({ball,
+                    std::make_shared<constant_medium>(std::make_shared<sphere>(vec3(150, 60, 150), 55.0, glass), 0.02,
+                                                      std::make_shared<isotropic>(solid(0.9, 0.9, 0.9))),
+                    std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(40, 40, 40), white),
+                                                vec3(60, 0, 60))}));
+        else
+            Add(L_({ball, std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(40, 40, 40), white),
+                                                      vec3(60, 0, 60))}));
+        if (media)
         Add(std::make_shared<translate>(
             L_({std::make_shared<constant_medium>(
                     std::make_shared<rotate_y>(std::make_shared<box>(vec3(0, 0, 0), vec3(100, 100, 100), white),
@@ -200,6 +205,10 @@ public:
                     L_({std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(50, 50, 50), red),
                                                     vec3(100, 350, 250))}),
                     20.0)}));
+        Add(std::make_shared<flip_normals>(
+            L_({std::make_shared<xz_rect>(400.0, 500.0, 50.0, 150.0, 500.0, white),
+                std::make_shared<translate>(std::make_shared<xz_rect>(0.0, 100.0, 0.0, 100.0, 0.0, green),
+                                            vec3(50, 520, 400))})));
         this->cam = camera(vec3(278.0, 278.0, -800.0), vec3(278.0, 278.0, 0.0), vec3(0.0, 1.0, 0.0), 40.0, aspect,
                            0.0, 10.0, 0.0, 1.0);
         this->background_type = BackgroundType::Black;
@@ -208,6 +217,7 @@ public:
 
 static scene* make_scene(const std::string& name, double aspect) {
     if (name == "nested") return new nested_scene(aspect);
+    if (name == "nested_plain") return new nested_scene(aspect, false);
     if (name == "cornell_box") return new cornell_box_scene(aspect);
     if (name == "random_balls") return new random_balls_scene(aspect);
     if (name == "dielectric") return new dielectric_scene(aspect);

@@ -59,11 +59,12 @@ public:
 // Test scene for arbitrary nesting (transforms and media inside lists).
 class nested_scene : public scene {
 public:
-    explicit nested_scene(double aspect);
+    explicit nested_scene(double aspect, bool media = true);
 };
 
 // Builds a scene by name ("cornell_box", "random_balls", "dielectric",
-// "light_sample", "book2_final", "nested"); nullptr for an unknown name.
+// "light_sample", "book2_final", "nested", "nested_plain"); nullptr for an
+// unknown name.
 std::unique_ptr<scene> make_builtin_scene(const std::string& name, double aspect);
 
 // Flatten the hittable graph of `sc` into a library-owned rtw_scene_desc

@@ -203,8 +203,10 @@ book2_final_scene::book2_final_scene(double aspect) {
 // same way in oracle/ref_harness.cpp from the reference's classes): the
 // Cornell room, then instanced boxes inside a list, a flip over a list
 // holding a transformed rect, a medium inside a nested list, a medium inside
-// a translated list, and lists two deep under rotate_y / translate.
-nested_scene::nested_scene(double aspect) {
+// a translated list, lists two deep under rotate_y / translate, and a flip
+// over a list holding a bare and a translated rect.  "nested_plain" drops
+// the media (world runs instead of the media walk).
+nested_scene::nested_scene(double aspect, bool media) {
     auto red = diffuse(0.65f, 0.05f, 0.05f);
     auto white = diffuse(0.73f, 0.73f, 0.73f);
     auto green = diffuse(0.12f, 0.45f, 0.15f);
@@ -239,12 +241,17 @@ nested_scene::nested_scene(double aspect) {
     // a medium inside a nested list (a glass ball full of fog)
     auto ball = std::make_shared<sphere>(vec3(150, 60, 150), 60.0, glass);
     lights->objects.push_back(ball);
-    Add(L_({ball,
-            std::make_shared<constant_medium>(std::make_shared<sphere>(vec3(150, 60, 150), 55.0, glass), 0.02,
-                                              std::make_shared<isotropic>(solid(0.9, 0.9, 0.9))),
-            std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(40, 40, 40), white),
-                                        vec3(60, 0, 60))}));
+    if (media)
+        Add(L_({ball,
+                std::make_shared<constant_medium>(std::make_shared<sphere>(vec3(150, 60, 150), 55.0, glass), 0.02,
+                                                  std::make_shared<isotropic>(solid(0.9, 0.9, 0.9))),
+                std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(40, 40, 40), white),
+                                            vec3(60, 0, 60))}));
+    else
+        Add(L_({ball, std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(40, 40, 40), white),
+                                                  vec3(60, 0, 60))}));
     // a medium inside a translated list
+    if (media)
     Add(std::make_shared<translate>(
         L_({std::make_shared<constant_medium>(
                 std::make_shared<rotate_y>(std::make_shared<box>(vec3(0, 0, 0), vec3(100, 100, 100), white), 20.0),
@@ -259,12 +266,19 @@ nested_scene::nested_scene(double aspect) {
                 L_({std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(50, 50, 50), red),
                                                 vec3(100, 350, 250))}),
                 20.0)}));
+    // a flip over a list of a bare rect and a translated one (the bare rect
+    // becomes an entry whose only op is the flip)
+    Add(std::make_shared<flip_normals>(
+        L_({std::make_shared<xz_rect>(400.0, 500.0, 50.0, 150.0, 500.0, white),
+            std::make_shared<translate>(std::make_shared<xz_rect>(0.0, 100.0, 0.0, 100.0, 0.0, green),
+                                        vec3(50, 520, 400))})));
     cam = look(vec3(278.0, 278.0, -800.0), vec3(278.0, 278.0, 0.0), 40.0, aspect, 0.0, 10.0);
     background_type = BackgroundType::Black;
 }
 
 std::unique_ptr<scene> make_builtin_scene(const std::string& name, double aspect) {
     if (name == "nested") return std::make_unique<nested_scene>(aspect);
+    if (name == "nested_plain") return std::make_unique<nested_scene>(aspect, false);
     if (name == "cornell_box") return std::make_unique<cornell_box_scene>(aspect);
     if (name == "random_balls") return std::make_unique<random_balls_scene>(aspect);
     if (name == "dielectric") return std::make_unique<dielectric_scene>(aspect);

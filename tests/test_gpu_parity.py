@@ -29,6 +29,8 @@ CASES = [
     # transforms and media inside nested lists (visit program, media frames)
     ("nested", 48, 36, 4, 50, False),
     ("nested", 40, 40, 3, 20, True),
+    ("nested_plain", 48, 36, 4, 50, False),
+    ("nested_plain", 48, 36, 4, 50, True),
 ]
 
 

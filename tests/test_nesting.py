@@ -115,10 +115,11 @@ def model(world):
     return entries, visits
 
 
-def test_nested_scene_flattens_as_modelled():
-    dump = json.loads((GOLD / "scene_nested.json").read_text())
+@pytest.mark.parametrize("name", ["nested", "nested_plain"])
+def test_nested_scene_flattens_as_modelled(name):
+    dump = json.loads((GOLD / f"scene_{name}.json").read_text())
     want_entries, want_visits = model(dump["world"])
-    sd = SceneDesc("nested", dump["aspect"])
+    sd = SceneDesc(name, dump["aspect"])
     d = sd.desc
     assert d.n_entries == len(want_entries)
     assert [d.visits[k] for k in range(d.n_visits)] == want_visits
@@ -145,6 +146,16 @@ def test_media_entries_keep_their_enclosing_frame():
     media = [d.entries[i] for i in range(d.n_entries) if d.entries[i].kind == _abi.RTW_ENTRY_MEDIUM]
     assert [(m.n_outer_ops, m.n_ops) for m in media] == [(0, 0), (1, 2)]
     assert media[1].op[0] == _abi.RTW_OP_TRANSLATE and media[1].op[1] == _abi.RTW_OP_ROTATE_Y
+
+
+def test_flip_over_a_list_gives_a_flip_only_entry():
+    """flip_normals over [rect, translate(rect)]: the bare rect becomes an
+    entry whose only op is the flip (world runs take it in: its ops leave the
+    ray alone), the translated one FLIP + TRANSLATE."""
+    d = SceneDesc("nested_plain", 1.0).desc
+    chains = [[d.entries[i].op[k] for k in range(d.entries[i].n_ops)] for i in range(d.n_entries)]
+    assert chains[-2:] == [[_abi.RTW_OP_FLIP], [_abi.RTW_OP_FLIP, _abi.RTW_OP_TRANSLATE]]
+    assert d.n_visits == 0  # no media: one walk over the entries
 
 
 @pytest.mark.parametrize("bad", ["visit", "outer"])
