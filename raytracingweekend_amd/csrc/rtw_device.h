@@ -789,7 +789,7 @@ RTW_D bvh_node32 node_at(const scene& S, int i) {
     using glb_v4 = const __attribute__((address_space(1))) v4u;
     v4u a, b;
     if (i < S.n_lnodes) {
-        lds_v4* p = (lds_v4*)(uint32_t)(uintptr_t)(S.lnodes + i);
+        lds_v4* p = (lds_v4*)(S.lnodes + i);
         a = p[0], b = p[1];
     } else {
         glb_v4* p = (glb_v4*)(S.nodes + i);

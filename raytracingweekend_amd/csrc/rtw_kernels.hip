@@ -1712,7 +1712,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
 
 // Shade kernels are instantiated for a few material/texture sets; a scene
 // runs the smallest instantiated superset of its own set.
-constexpr int kShadeMasks[] = {SF_DIEL, SF_METAL | SF_DIEL, SF_NOISE, SF_ALL};
+constexpr int SF_NOCHECKER = SF_ALL & ~SF_CHECKER;  // the Book-2 set: noise, metal, glass, media
+constexpr int kShadeMasks[] = {SF_DIEL, SF_METAL | SF_DIEL, SF_NOISE, SF_NOCHECKER, SF_ALL};
 
 constexpr uint32_t kShadeLdsMax = 40 * 1024;
 
@@ -1890,6 +1891,10 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     RTW_PER(F_YSPH, SF_METAL | SF_DIEL, false)
     RTW_PER(F_WBVH | F_NOLIGHTS, SF_METAL | SF_DIEL, false)
     RTW_PER(F_WBVH, SF_METAL | SF_DIEL, false)
+    // media scenes without checker textures (Book 2): the checker's sines
+    // and texture recursion compiled out halves the kernel's SGPR spills
+    RTW_PER(F_MEDIA | F_GBVH, SF_NOCHECKER, false)
+    RTW_PER(F_MEDIA, SF_NOCHECKER, false)
 #else
     // experiment builds (scripts/ru_kernel.sh): one persistent kernel only
     RTW_PER(RTW_SUBSET_F, RTW_SUBSET_M, RTW_SUBSET_L)
