@@ -628,7 +628,8 @@ struct ray_batch {  // one wave's buffer of generated camera samples (LDS)
 #ifdef RTW_SEG_WAVES
 #define RTW_PERSIST_WAVES(F, M) RTW_SEG_WAVES
 #else
-#define RTW_PERSIST_WAVES(F, M) (((F) & F_BLACK) || (((F) & F_YSPH) && (M) != SF_ALL) ? 5 : 4)
+#define RTW_PERSIST_WAVES(F, M)                                                                        \
+    ((((F) & F_BLACK) && !((F) & (F_MEDIA | F_WBVH | F_GBVH))) || (((F) & F_YSPH) && (M) != SF_ALL) ? 5 : 4)
 #endif
 // The persistent kernels' one argument.
 struct persist_args {
@@ -790,7 +791,8 @@ void k_persist(persist_args) {
                 },
                 [&](const d3& E) { radiance(d3{s_thr[0][me], s_thr[1][me], s_thr[2][me]} * E); },
                 [&]() { radiance(d3{0, 0, 0}); });
-            const int out = shade_core<M, false, false, false, (F & F_NOLIGHTS) != 0>(SS, x, h.t, h.prim, sk, pf);
+            const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0,
+                                       (F & F_NOLIGHTS) != 0>(SS, x, h.t, h.prim, sk, pf);
             if (out == SEG_CONTINUE)
                 x.r = nr;
             else
@@ -1869,8 +1871,7 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     if (ysph && !(f & (F_WBVH | F_MEDIA))) f |= F_YSPH;  // world runs are walked: y-sphere scans
     const int pick = pick_shade_mask(mask);
     // specialised kernels only
-    const int fs = f | (static_scene ? F_STATIC : 0) | (static_scene && lights ? F_LIGHTS : 0) |
-                   (static_scene && lights && black ? F_BLACK : 0) | (lights ? 0 : F_NOLIGHTS);
+    const int fs = f | (static_scene ? F_STATIC : 0) | (lights ? F_LIGHTS : F_NOLIGHTS) | (black ? F_BLACK : 0);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
 #define RTW_PER(FF, MM, LL)                                                                     \
@@ -1893,6 +1894,7 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     RTW_PER(F_WBVH, SF_METAL | SF_DIEL, false)
     // media scenes without checker textures (Book 2): the checker's sines
     // and texture recursion compiled out halves the kernel's SGPR spills
+    RTW_PER(F_MEDIA | F_GBVH | F_LIGHTS | F_BLACK, SF_NOCHECKER, false)
     RTW_PER(F_MEDIA | F_GBVH, SF_NOCHECKER, false)
     RTW_PER(F_MEDIA, SF_NOCHECKER, false)
 #else
