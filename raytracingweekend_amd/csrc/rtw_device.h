@@ -34,6 +34,21 @@ constexpr double kCanonDiv = 4611686009837453312.0;
 constexpr double kCanonR = 2147483646.0;
 constexpr double kCanonRcp = 1.0 / kCanonDiv;  // RN(1/x): constant folding is IEEE
 
+// A value materialised where it is used (an opaque VGPR copy the compiler can
+// neither hoist out of a loop nor merge with another use): 64-bit constants
+// the persistent kernels need inside their loop (the initial closest t, a
+// zero radiance) are otherwise held in VGPR pairs across the whole loop and
+// spilled to scratch.
+// (The two v_mov are emitted by the asm itself: an opaque copy of a
+// constant would still be fed from the loop-carried register.)
+template <uint64_t B>
+__device__ __forceinline__ double in_place() {
+    uint32_t lo, hi;
+    asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(lo), "=v"(hi) : "i"((uint32_t)B), "i"((uint32_t)(B >> 32)));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+constexpr uint64_t kDblMaxBits = 0x7FEFFFFFFFFFFFFFull;  // == kDblMax
+
 // ------------------------------------------------------------------ vec3
 struct d3 {
     double x, y, z;
@@ -915,7 +930,7 @@ RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_mi
 // media's fresh draws, so it re-evaluates just the media, in list order.
 template <int F, class STK>
 RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& stk) {
-    hit_state h{kDblMax, -1, false};
+    hit_state h{in_place<kDblMaxBits>(), -1, false};
     if constexpr ((F & F_WBVH) != 0 && (F & F_MEDIA) == 0) {
         const double fc = motion_frac(S, r.t, S.mv_common != 0);  // transforms keep the ray's time
         const slab_ray sr = make_slab_ray(S, r);
@@ -1127,6 +1142,7 @@ RTW_D d3 texture_value(const scene& S, int id, d3 p) {
 }
 
 // ------------------------------------------------------------------ lights
+template <bool STATIC>
 RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
     if (L.kind == RTW_LIGHT_XZ_RECT) {  // hittable.h:208-222
         const rtw_prim& q = S.prims[L.prim];
@@ -1142,7 +1158,8 @@ RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
         const rtw_prim& q = S.prims[L.prim];
         const ray r{o, v, kFltMax};
         double t;
-        if (!sphere_t(q, r, 0.001, __builtin_inf(), t, motion_frac(S, r.t, q.type >= DP_MOVING_COMMON)))
+        // (STATIC: no moving spheres, the fraction is never read)
+        if (!sphere_t(q, r, 0.001, __builtin_inf(), t, STATIC ? 0.0 : motion_frac(S, r.t, q.type >= DP_MOVING_COMMON)))
             return 0.0;
         const double cos_theta_max = __builtin_sqrt(1 - q.p[9] / len2(ld3(q.p) - o));  // p[9] = radius * radius
         const double solid_angle = kTwoPi * (1.0 - cos_theta_max);
@@ -1215,10 +1232,11 @@ RTW_D d3 mixture_generate(const scene& S, const surf_frame& sf, d3 o, uint32_t& 
     return local(frame_onb(S, bf), d3{cp * sq, sp * sq, z});
 }
 
+template <bool STATIC = false>
 RTW_D double lights_pdf_value(const scene& S, d3 o, d3 v) {  // hittable_list.h:44-53
     const double weight = S.light_weight;  // 1.0 / (double)n_lights, computed once on the host
     double sum = 0.0;
-    for (int i = 0; i < S.n_lights; ++i) sum += weight * light_pdf_value(S, S.lights[i], o, v);
+    for (int i = 0; i < S.n_lights; ++i) sum += weight * light_pdf_value<STATIC>(S, S.lights[i], o, v);
     return sum;
 }
 

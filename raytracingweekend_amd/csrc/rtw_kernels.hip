@@ -441,7 +441,7 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
             const double cw = dot(ud, frame_w(S, sf));
             cosine = dot(n, ud);  // material.h:115-119
             const double p0 = (cw <= 0) ? 0 : cw / kPi;
-            pdf_val = 0.5 * p0 + 0.5 * lights_pdf_value(S, p, dir);
+            pdf_val = 0.5 * p0 + 0.5 * lights_pdf_value<STATIC>(S, p, dir);
         } else {
             dir = local(frame_onb(S, sf), random_cosine_direction(rng));
             const d3 ud = normalize(dir);
@@ -790,7 +790,10 @@ void k_persist(persist_args) {
                     nr = r;
                 },
                 [&](const d3& E) { radiance(d3{s_thr[0][me], s_thr[1][me], s_thr[2][me]} * E); },
-                [&]() { radiance(d3{0, 0, 0}); });
+                [&]() {
+                    const double z = in_place<0>();
+                    radiance(d3{z, z, z});
+                });
             const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0,
                                        (F & F_NOLIGHTS) != 0>(SS, x, h.t, h.prim, sk, pf);
             if (out == SEG_CONTINUE)
@@ -1019,7 +1022,10 @@ void k_persist_sort(persist_args) {
                     const uint32_t home = x_home[me];
                     radiance(d3{s_thr[0][home], s_thr[1][home], s_thr[2][home]} * E);
                 },
-                [&]() { radiance(d3{0, 0, 0}); });
+                [&]() {
+                    const double z = in_place<0>();
+                    radiance(d3{z, z, z});
+                });
             const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0,
                                        (F & F_NOLIGHTS) != 0>(SS, x, x_t[me], x_prim[me], sk, pf);
             if (out != SEG_CONTINUE) x.depth = 0;
