@@ -49,6 +49,36 @@ __device__ __forceinline__ double in_place() {
 }
 constexpr uint64_t kDblMaxBits = 0x7FEFFFFFFFFFFFFFull;  // == kDblMax
 
+// ------------------------------------------------------------------ libm
+// sin of the textures (texture.h:45, :66) and log of the media (hittable.h:
+// 450): rtw_math.h's sin_wide / log_pos (within an ulp of glibc's, which the
+// reference calls) in their ranges, ocml's functions in separate functions
+// beyond.  ocml's inlined sin and log hold fifteen 64-bit polynomial
+// constants the media kernels kept in VGPR pairs across their loop and
+// spilled; log_pos reads its constants from a table where it runs.
+__device__ __attribute__((noinline)) double sin_far(double x) { return sin(x); }
+__device__ __attribute__((noinline)) double log_far(double x) { return log(x); }
+RTW_D double sin_tex(double x) {
+    double s = sin_wide(x);
+    if (__builtin_expect(!sin_wide_ok(x), 0)) {
+        asm volatile("");
+        s = sin_far(x);
+    }
+    return s;
+}
+__constant__ double c_log_coef[9] = {kLogCoef[0], kLogCoef[1], kLogCoef[2], kLogCoef[3], kLogCoef[4],
+                                     kLogCoef[5], kLogCoef[6], kLogCoef[7], kLogCoef[8]};
+RTW_D double log_dev(double x) {
+    const __attribute__((address_space(4))) double* t = (const __attribute__((address_space(4))) double*)c_log_coef;
+    asm volatile("" : "+s"(t));  // the table's loads are issued here, not hoisted
+    double l = log_pos(x, [&](int i) { return t[i]; });
+    if (__builtin_expect(!log_pos_ok(x), 0)) {
+        asm volatile("");
+        l = log_far(x);
+    }
+    return l;
+}
+
 // ------------------------------------------------------------------ vec3
 struct d3 {
     double x, y, z;
@@ -915,7 +945,7 @@ RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_mi
     if (t1 < 0) t1 = 0;
     const double dl = len(r.d);
     const double inside = (t2 - t1) * dl;
-    const double hit_distance = -(1 / rd<true>(&e.p->density)) * log(rnd01(rng));
+    const double hit_distance = -(1 / rd<true>(&e.p->density)) * log_dev(rnd01(rng));
     if (hit_distance < inside) {
         t_out = t1 + hit_distance / dl;
         return true;
@@ -1084,6 +1114,7 @@ RTW_D void hit_record(const scene& S, const ray& r, const hit_state& h, d3& p, d
 }
 
 // ------------------------------------------------------------------ textures
+
 RTW_D double smooth(double x) { return x * x * (3 - 2 * x); }  // noise.h:9-12
 
 RTW_D double perlin_noise(const scene& S, d3 p) {  // noise.h:89-151 (PERLIN branch)
@@ -1127,13 +1158,13 @@ RTW_D d3 texture_value(const scene& S, int id, d3 p) {
         const rtw_texture& t = S.textures[id];
         if (!(M & (SF_NOISE | SF_CHECKER)) || t.type == RTW_TEX_CONSTANT) return ld3(t.color);
         if ((M & SF_CHECKER) && t.type == RTW_TEX_CHECKER) {  // texture.h:38-49
-            const double sines = sin(10.0 * p.x) * sin(10.0 * p.y) * sin(10.0 * p.z);
+            const double sines = sin_tex(10.0 * p.x) * sin_tex(10.0 * p.y) * sin_tex(10.0 * p.z);
             id = sines < 0 ? t.odd : t.even;
             continue;
         }
         if (M & SF_NOISE) {
             // texture.h:57-68: vec3(1,1,1) * 0.5f * (1 + sin(scale*p.z + 10*turb(p)))
-            const double v = (1.0 * (double)0.5f) * (1 + sin(t.scale * p.z + 10 * turb(S, p)));
+            const double v = (1.0 * (double)0.5f) * (1 + sin_tex(t.scale * p.z + 10 * turb(S, p)));
             return d3{v, v, v};
         }
         return ld3(t.color);

@@ -2,6 +2,7 @@
 // tests (tests/cpp/sincos_check.cpp).
 #pragma once
 
+#include <stdint.h>
 #if defined(__HIPCC__)
 #define RTW_HD __host__ __device__ __forceinline__
 #else
@@ -53,6 +54,62 @@ RTW_HD void sincos_azimuth(double x, double& sn, double& cs) {
     const double c0 = (q & 1) ? sr : cr;
     sn = (q & 2) ? -s0 : s0;
     cs = ((q + 1) & 2) ? -c0 : c0;
+}
+
+// sin(x) for |x| <= 2^19 (sin_wide_ok) with sincos_azimuth's reduction and
+// kernel: n = rint(x * 2/pi) stays below 2^19, so n * pio2_1 and n * pio2_2
+// (33 significant bits each) are still exact and the remainder carries 119
+// bits of pi/2.  Within an ulp of glibc's sin over that range
+// (tests/cpp/sincos_check.cpp); callers take their own path outside it.
+RTW_HD bool sin_wide_ok(double x) { return __builtin_fabs(x) <= 0x1p19; }
+RTW_HD double sin_wide(double x) {
+    double s, c;
+    sincos_azimuth(x, s, c);
+    return s;
+}
+
+// log(x) for x positive, normal and finite (log_pos_ok): fdlibm's
+// __ieee754_log (e_log.c, < 1 ulp).  x = 2^k (1 + f) with 1 + f in
+// [sqrt(2)/2, sqrt(2)), s = f / (2 + f), log(1 + f) = f - (hfsq - s (hfsq + R))
+// with R(s^2) a degree-14 polynomial; fdlibm's k == 0 forms are the same
+// arithmetic with the exact zero terms left out, so one form serves all k.
+// The constants come from coef(i) (i = 0 ln2_hi, 1 ln2_lo, 2..8 Lg1..Lg7):
+// the device reads them from a table where the log is evaluated, so they are
+// not held in registers across a kernel's loop.  Within an ulp of glibc's
+// log (tests/cpp/sincos_check.cpp).
+constexpr double kLogCoef[9] = {
+    6.93147180369123816490e-01, 1.90821492927058770002e-10, 6.666666666666735130e-01, 3.999999999940941908e-01,
+    2.857142874366239149e-01,   2.222219843214978396e-01,   1.818357216161805012e-01, 1.531383769920937332e-01,
+    1.479819860511658591e-01};
+RTW_HD bool log_pos_ok(double x) { return x >= 0x1p-1022 && x <= 1.7976931348623157e308; }
+template <class C>
+RTW_HD double log_pos(double x, C coef) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    int32_t hx = (int32_t)(b >> 32);
+    int k = (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    const int32_t i = (hx + 0x95f64) & 0x100000;
+    const uint64_t nb = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (b & 0xffffffffull);
+    k += i >> 20;
+    const double f = __builtin_bit_cast(double, nb) - 1.0;  // x or x/2 normalised, minus 1
+    const double dk = (double)k;
+    if ((0x000fffff & (2 + hx)) < 3) {  // -2^-20 <= f < 2^-20
+        if (f == 0.0) return k == 0 ? 0.0 : dk * coef(0) + dk * coef(1);
+        const double R = f * f * (0.5 - 0.33333333333333333 * f);
+        return dk * coef(0) - ((R - dk * coef(1)) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double w = z * z;
+    const int32_t ii = (hx - 0x6147a) | (0x6b851 - hx);
+    const double t1 = w * (coef(3) + w * (coef(5) + w * coef(7)));
+    const double t2 = z * (coef(2) + w * (coef(4) + w * (coef(6) + w * coef(8))));
+    const double R = t2 + t1;
+    if (ii > 0) {
+        const double hfsq = 0.5 * f * f;
+        return dk * coef(0) - ((hfsq - (s * (hfsq + R) + dk * coef(1))) - f);
+    }
+    return dk * coef(0) - ((s * (f - R) - dk * coef(1)) - f);
 }
 
 }  // namespace rtwd

@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <initializer_list>
 #include "rtw_math.h"
 
 static double ulp_diff(double a, double b) {
@@ -41,6 +42,43 @@ int main(int argc, char** argv) {
             ams = std::fmax(ams, std::fabs(s - std::sin(x)));
             amc = std::fmax(amc, std::fabs(c - std::cos(x)));
         }
-    std::printf("max_ulp_sin %.3f max_ulp_cos %.3f max_abs_sin %.3g max_abs_cos %.3g\n", ms, mc, ams, amc);
+    // sin_wide over [-2^19, 2^19] (the marble texture's argument): random
+    // arguments at every scale and the doubles next to multiples of pi / 2
+    double mw = 0;
+    for (long k = 0; k <= n; ++k) {
+        st = st * 6364136223846793005ull + 1442695040888963407ull;
+        const int e = (int)((st >> 40) % 40) - 20;  // |x| in [2^-20, 2^19]
+        double x = std::ldexp(1.0 + (double)(st >> 12 & 0xFFFFFFFFFFFull) * 0x1p-44, e);
+        if (x > 0x1p19) x = 0x1p19;
+        if (st & 1) x = -x;
+        mw = std::fmax(mw, ulp_diff(rtwd::sin_wide(x), std::sin(x)));
+    }
+    for (long m = 1; m <= 333772; m += (m < 4096 ? 1 : 97)) {  // m * pi/2 <= 2^19
+        const double c = m * (two_pi / 4);
+        for (double x : {c, std::nextafter(c, 0.0), std::nextafter(c, INFINITY)}) {
+            if (!rtwd::sin_wide_ok(x)) continue;
+            mw = std::fmax(mw, ulp_diff(rtwd::sin_wide(x), std::sin(x)));
+            mw = std::fmax(mw, ulp_diff(rtwd::sin_wide(-x), std::sin(-x)));
+        }
+    }
+    // log_pos over the media's arguments (canonical draws in [2^-62, 1)) and
+    // over every binade of the normal range
+    double ml = 0;
+    auto lc = [](int i) { return rtwd::kLogCoef[i]; };
+    for (long k = 0; k <= n; ++k) {
+        st = st * 6364136223846793005ull + 1442695040888963407ull;
+        const double u = (double)(st >> 11) * 0x1p-53;
+        const double x1 = u > 0x1p-62 ? u : 0x1p-62;
+        ml = std::fmax(ml, ulp_diff(rtwd::log_pos(x1, lc), std::log(x1)));
+        const int e = (int)((st >> 20) % 2046) - 1022;
+        const double x2 = std::ldexp(1.0 + (double)(st & 0xFFFFFFFFFFFFFull) * 0x1p-52, e);
+        if (rtwd::log_pos_ok(x2)) ml = std::fmax(ml, ulp_diff(rtwd::log_pos(x2, lc), std::log(x2)));
+        const double x3 = 1.0 + ((double)(st >> 11) * 0x1p-53 - 0.5) * 0x1p-18;  // near 1 (the small-f form)
+        ml = std::fmax(ml, ulp_diff(rtwd::log_pos(x3, lc), std::log(x3)));
+    }
+    for (double x : {1.0, 2.0, 0.5, 0x1p-1022, 1.7976931348623157e308, std::nextafter(1.0, 0.0), 0x1p-62})
+        ml = std::fmax(ml, ulp_diff(rtwd::log_pos(x, lc), std::log(x)));
+    std::printf("max_ulp_sin %.3f max_ulp_cos %.3f max_abs_sin %.3g max_abs_cos %.3g max_ulp_sin_wide %.3f "
+                "max_ulp_log %.3f\n", ms, mc, ams, amc, mw, ml);
     return 0;
 }

@@ -1,8 +1,9 @@
 """The device's azimuth sincos (rtw_math.h: fdlibm-style reduction and
 kernels, used for the 2*pi*r1 angle of the cosine and sphere-light samplers)
 is within 1 ulp of glibc's sin/cos -- the functions the reference calls --
-over [0, 2*pi], including next to the quadrant boundaries
-(tests/cpp/sincos_check.cpp)."""
+over [0, 2*pi], including next to the quadrant boundaries; so is its sine
+over [-2^19, 2^19] (sin_wide, the marble texture's sin), including the
+doubles next to multiples of pi/2 (tests/cpp/sincos_check.cpp)."""
 import subprocess
 from pathlib import Path
 
@@ -16,3 +17,4 @@ def test_sincos_azimuth_within_one_ulp_of_glibc(tmp_path):
     out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True, check=True).stdout.split()
     vals = dict(zip(out[0::2], map(float, out[1::2])))
     assert vals["max_ulp_sin"] <= 1.0 and vals["max_ulp_cos"] <= 1.0, vals
+    assert vals["max_ulp_sin_wide"] <= 1.0, vals
