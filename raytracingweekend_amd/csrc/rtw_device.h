@@ -697,7 +697,7 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
 // (Shared-reciprocal rect tests, as in group_scan's world walks, measured
 // −0.8 % C3 / −0.6 % C5 here: not used.)
 RTW_D void arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_state& h, double fc) {
-    const rtw_prim q = S.prims[pi];
+    const rtw_prim& q = S.prims[pi];  // fields read where the test uses them
     const bool rl = !is_sphere(q.type);
     double t;
     if (rl) {
@@ -716,7 +716,7 @@ RTW_D void arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_sta
 // 1 / dot(d, d) (walk_quot's rules; t_min = 0.001)
 RTW_D void arbitrate_a(const scene& S, int pi, const ray& r, double t_min, hit_state& h, double fc, double ya,
                        bool oka) {
-    const rtw_prim q = S.prims[pi];
+    const rtw_prim& q = S.prims[pi];
     const bool rl = !is_sphere(q.type);
     double t;
     if (rl) {

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU suite on the working tree, then interleaved A/B of the in-tree library
-# against _build/librtw_base.so (HEAD kernels) on T and a C5 slice.
+# against _build/librtw_base.so (HEAD kernels) on T, a C5 slice and a C3 slice.
 #   scripts/ab_quick.sh <tag> <rounds> [--no-tests]
 set -e
 tag=$1; rounds=$2
@@ -12,7 +12,7 @@ if [ "$3" != "--no-tests" ]; then
 fi
 for r in $(seq 1 "$rounds"); do
     for lib in default raytracingweekend_amd/_build/librtw_base.so; do
-        for w in "--workload T" "--workload C5 --spp 64" ${AB_EXTRA:+"$AB_EXTRA"}; do
+        for w in "--workload T" "--workload C5 --spp 64" "--workload C3 --spp 256"; do
             if [ "$lib" = default ]; then unset RTW_LIBRARY; else export RTW_LIBRARY=$lib; fi
             v=$(timeout -k 10 300 python bench.py $w --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-times | grep -o '"value": [0-9.]*')
             echo "round $r $lib $w $v" | tee -a gpurun_out/ab_$tag.log
