@@ -863,6 +863,10 @@ RTW_D void push_children(const bvh_node32& nd, int dneg, STK& stk, int& sp) {
     stk.at(sp++) = left_first ? nd.a : right;
 }
 
+#ifndef RTW_CHILD_TEST
+#define RTW_CHILD_TEST 1
+#endif
+
 RTW_D double widen_lo(double t) { return t > 0 ? t * 0.5 : t * 2.0 - 1e-9; }
 RTW_D double widen_hi(double t) { return t * (1 + 1e-12) + 1e-9; }
 
@@ -994,7 +998,52 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                 }
             }
         };
-        if constexpr ((F & F_GBVH) == 0) {
+        if constexpr ((F & F_GBVH) == 0 && RTW_CHILD_TEST) {
+            // Children tested by their parent's iteration: expanding an inner
+            // node loads both children and slab-tests them together; a lane
+            // continues with the nearer child that passes and stacks the
+            // other, so a child whose box fails costs no iteration of its
+            // own.  A stacked node's box is tested again when it is popped
+            // (the closest hit may have tightened since).  While-while as
+            // below: lanes run inner iterations until each holds a leaf.
+            int ca = 0, cb = 0;  // the node this lane expands next: its a / b fields
+            bool have = false;
+            {
+                const bvh_node32 rt = node_at(S, S.world_bvh_root);
+                if (slab32(rt, sr, t0, (float)widen_hi(h.t))) ca = rt.a, cb = rt.b, have = true;
+            }
+            sp = 0;
+            for (;;) {
+                int la = 0, lc = 0;  // this lane's pending leaf: first item, count
+                while (lc == 0) {
+                    if (!have) {
+                        if (sp == 0) break;
+                        const bvh_node32 nd = node_at(S, stk.at(--sp));
+                        if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
+                        ca = nd.a, cb = nd.b, have = true;
+                    }
+                    if (cb < 0) {  // a leaf
+                        la = ca, lc = -cb, have = false;
+                        break;
+                    }
+                    const int pad = cb >> 28, right = cb & 0x0fffffff;
+                    const bvh_node32 L = node_at(S, ca), R = node_at(S, right);
+                    const float t1 = (float)widen_hi(h.t);
+                    const bool hl = slab32(L, sr, t0, t1), hr = slab32(R, sr, t0, t1);
+                    const bool left_first = (((dneg >> (pad & 3)) ^ (pad >> 2)) & 1) == 0;
+                    const bool hn = left_first ? hl : hr, hf = left_first ? hr : hl;
+                    const int far_i = left_first ? right : ca;
+                    const int na = left_first ? L.a : R.a, nb = left_first ? L.b : R.b;
+                    const int fa = left_first ? R.a : L.a, fb = left_first ? R.b : L.b;
+                    if (hn && hf && sp + 1 <= STK::cap) stk.at(sp++) = far_i;  // always fits: depth checked at upload
+                    have = hn || hf;
+                    ca = hn ? na : fa;
+                    cb = hn ? nb : fb;
+                }
+                if (lc == 0) break;
+                leaf(la, lc);
+            }
+        } else if constexpr ((F & F_GBVH) == 0) {
             // while-while: each lane walks inner nodes until it reaches a
             // leaf that passes its slab test (or its stack runs dry), then
             // all lanes test their leaves together, so the leaf code runs
