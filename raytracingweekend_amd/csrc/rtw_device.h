@@ -632,6 +632,10 @@ RTW_D double walk_quot(double num, double den, double y, bool ok) {
 // with c0.y != 0, whose p[5] it sets to 0 (c0.y + 0 * fc == c0.y exactly,
 // fc finite), so one branch-free body serves the whole run: the Book-1
 // random_balls list.  Same arithmetic as sphere.h:46-81 per sphere.
+#ifndef RTW_YS_AHEAD
+#define RTW_YS_AHEAD 4
+#endif
+constexpr int kYsAhead = RTW_YS_AHEAD;  // fp32 records in flight ahead of the filtered one
 RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, double fc) {
     const double a = dot(r.d, r.d);
     const bool oka = walk_ray_ok(S, r, fc) && div_hw_ok_b(a);  // world walk: t_min = 0.001
@@ -652,40 +656,53 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
     const float R1 = __builtin_fabsf(oyf) + __builtin_fmaf(S.ysb_dy, __builtin_fabsf(fcf), S.ysb_cy);
     const float R2 = __builtin_fabsf(ozf) + S.ysb_cz;
     const float E = 0x1p-16f * af * (R0 * R0 + R1 * R1 + R2 * R2 + S.ysb_r2) + 0x1p-60f;  // + denormal slack
-    // software-pipelined scalar loads of the fp32 records: sphere i+1's is
-    // requested before sphere i is filtered
-    const float* f = S.ysph + 8 * (size_t)first;
-    float cx = ld(f), cy = ld(f + 1), cz = ld(f + 2), dy = ld(f + 3), rr = ld(f + 4);
-    for (int i = 0; i < n; ++i) {
-        const float* fn = S.ysph + 8 * (size_t)(first + (i + 1 < n ? i + 1 : i));
-        const float nx = ld(fn), ny = ld(fn + 1), nz = ld(fn + 2), ndy = ld(fn + 3), nrr = ld(fn + 4);
-        const float ocx = oxf - cx, ocy = oyf - __builtin_fmaf(dy, fcf, cy), ocz = ozf - cz;
-        const float b32 = __builtin_fmaf(ocx, dxf, __builtin_fmaf(ocy, dyf, ocz * dzf));
-        const float q32 = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
-        const float d32 = __builtin_fmaf(b32, b32, -(af * (q32 - rr)));
-        if (__builtin_amdgcn_ballot_w64(!(d32 <= -E))) {
-            // the reference's test, sphere.h:46-81 (exact fp64)
-            const double* p = S.prims[first + i].p;
-            const d3 oc{r.o.x - ld(p), r.o.y - (ld(p + 1) + ld(p + 5) * fc), r.o.z - ld(p + 2)};
-            const double b = dot(oc, r.d);
-            const double c = dot(oc, oc) - ld(p + 9);
-            const double disc = b * b - a * c;
-            if (disc > 0) {
-                const double sq = __builtin_sqrt(disc);
-                double temp = walk_quot(-b - sq, a, ya, oka);
-                bool ok = temp < h.t && temp > t_min;
-                if (!ok) {
-                    temp = walk_quot(-b + sq, a, ya, oka);
-                    ok = temp < h.t && temp > t_min;
-                }
-                if (ok) {
-                    h.t = temp;
-                    h.prim = first + i;
-                    h.rect = false;
+    // software-pipelined scalar loads of the fp32 records: the records of
+    // the next kYsAhead spheres are in flight while sphere i is filtered (a
+    // ring of registers, the loop unrolled by its length)
+    struct ysrec {
+        float cx, cy, cz, dy, rr;
+    };
+    auto load = [&](int i) {
+        const float* g = S.ysph + 8 * (size_t)(first + (i < n ? i : n - 1));
+        return ysrec{ld(g), ld(g + 1), ld(g + 2), ld(g + 3), ld(g + 4)};
+    };
+    ysrec ring[kYsAhead];
+#pragma unroll
+    for (int j = 0; j < kYsAhead; ++j) ring[j] = load(j);
+    for (int i0 = 0; i0 < n; i0 += kYsAhead) {
+#pragma unroll
+        for (int j = 0; j < kYsAhead; ++j) {
+            const int i = i0 + j;
+            if (i >= n) break;
+            const ysrec cur = ring[j];
+            ring[j] = load(i + kYsAhead);
+            const float ocx = oxf - cur.cx, ocy = oyf - __builtin_fmaf(cur.dy, fcf, cur.cy), ocz = ozf - cur.cz;
+            const float b32 = __builtin_fmaf(ocx, dxf, __builtin_fmaf(ocy, dyf, ocz * dzf));
+            const float q32 = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
+            const float d32 = __builtin_fmaf(b32, b32, -(af * (q32 - cur.rr)));
+            if (__builtin_amdgcn_ballot_w64(!(d32 <= -E))) {
+                // the reference's test, sphere.h:46-81 (exact fp64)
+                const double* p = S.prims[first + i].p;
+                const d3 oc{r.o.x - ld(p), r.o.y - (ld(p + 1) + ld(p + 5) * fc), r.o.z - ld(p + 2)};
+                const double b = dot(oc, r.d);
+                const double c = dot(oc, oc) - ld(p + 9);
+                const double disc = b * b - a * c;
+                if (disc > 0) {
+                    const double sq = __builtin_sqrt(disc);
+                    double temp = walk_quot(-b - sq, a, ya, oka);
+                    bool ok = temp < h.t && temp > t_min;
+                    if (!ok) {
+                        temp = walk_quot(-b + sq, a, ya, oka);
+                        ok = temp < h.t && temp > t_min;
+                    }
+                    if (ok) {
+                        h.t = temp;
+                        h.prim = first + i;
+                        h.rect = false;
+                    }
                 }
             }
         }
-        cx = nx, cy = ny, cz = nz, dy = ndy, rr = nrr;
     }
 }
 
