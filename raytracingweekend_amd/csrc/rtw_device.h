@@ -997,6 +997,10 @@ RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_mi
     return false;
 }
 
+#ifdef RTW_PROF_WALK
+__device__ unsigned long long g_walk[32][64];  // clock per media-walk position (sampled walks), per lane slot
+#endif
+
 // World closest hit (hittable_list::hit hittable_list.h:11-37).  Without
 // media, one walk in list order equals the reference's two walks (every
 // primitive is deterministic; the second walk re-accepts only what the first
@@ -1111,6 +1115,10 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             // the media walk: entries in the order the reference's nested
             // list walks call them (scene::media; with media the run form
             // spills more registers than it saves, measured on Book-2 BVH)
+#ifdef RTW_PROF_WALK  // profiling builds: clock per visit of the media walk, by entry (g_walk)
+            const bool pw = (rng & 63) == 0;  // a sample of the walks
+            uint64_t pw_t = pw ? clock64() : 0;
+#endif
             for (int k = 0; k < S.n_media; ++k) {
                 const int ei = ld(&S.media[k]);
                 const entry_v e = view_entry<true>(S, ei);
@@ -1121,10 +1129,17 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                         h.prim = -(2 + ei);
                         h.rect = false;
                     }
-                    continue;
+                } else {
+                    const ray lr = entry_local_ray<true>(e, r);
+                    group_closest<F>(S, e, lr, kTMin, h, stk);
                 }
-                const ray lr = entry_local_ray<true>(e, r);
-                group_closest<F>(S, e, lr, kTMin, h, stk);
+#ifdef RTW_PROF_WALK
+                if (pw) {
+                    const uint64_t now = clock64();
+                    atomicAdd(&g_walk[k < 31 ? k : 31][threadIdx.x & 63], (unsigned long long)(now - pw_t));
+                    pw_t = now;
+                }
+#endif
             }
         } else {
             for (int ri = 0; ri < S.n_runs; ++ri) {

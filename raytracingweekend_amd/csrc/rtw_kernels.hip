@@ -2504,6 +2504,19 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         HIPCHK(hipEventElapsedTime(&ms, h->events[p.first], h->events[p.second]));
         stats.ms_shade += ms;
     }
+#ifdef RTW_PROF_WALK
+    {
+        static unsigned long long w[32][64];
+        HIPCHK(hipMemcpyFromSymbol(w, HIP_SYMBOL(g_walk), sizeof w));
+        std::fprintf(stderr, "[rtw walk] sampled clock by media-walk position:");
+        for (int k = 0; k < 32; ++k) {
+            unsigned long long t = 0;
+            for (int l = 0; l < 64; ++l) t += w[k][l];
+            if (t) std::fprintf(stderr, " %d:%llu", k, t);
+        }
+        std::fprintf(stderr, "\n");
+    }
+#endif
 #ifdef RTW_PROF
     {
         unsigned long long pr[PS_N];
