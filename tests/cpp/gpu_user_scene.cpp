@@ -1,6 +1,7 @@
 // GPU parity for a user scene that exercises what the built-in scenes leave
 // out (compiled and run by tests/test_gpu_parity.py on the GPU box):
-// checker texture (texture.h:38-49), metal with fuzz (material.h:128-136),
+// checker texture (texture.h:38-49), a marble texture whose sine argument
+// crosses 2^19 (texture.h:57-68), metal with fuzz (material.h:128-136),
 // hollow glass (negative radius, sphere.h:71-77), nested translate/rotate_y/
 // flip_normals, a moving sphere, a constant medium, lights of all three
 // kinds (xz_rect, sphere, and a box = hittable default pdf), gradient
@@ -37,6 +38,10 @@ public:
         Add(std::make_shared<sphere>(vec3(0, 1, 0), -0.9, glass));  // hollow glass shell
         lights->objects.push_back(ball);
         Add(std::make_shared<sphere>(vec3(-2.2, 0.7, 0.5), 0.7, fuzzy));
+        // marble with a huge scale: sin(scale * p.z + 10 turb) runs both the
+        // device's sin_wide (|x| <= 2^19) and its ocml fallback beyond
+        Add(std::make_shared<sphere>(vec3(1.2, 0.5, -1.0), 0.5,
+                                     std::make_shared<lambertian>(std::make_shared<noise_texture>(1.0e6))));
         Add(std::make_shared<translate>(
             std::make_shared<rotate_y>(
                 std::make_shared<translate>(std::make_shared<box>(vec3(0, 0, 0), vec3(1, 2, 1), mirror),
