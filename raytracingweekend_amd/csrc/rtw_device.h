@@ -635,6 +635,9 @@ RTW_D double walk_quot(double num, double den, double y, bool ok) {
 #ifndef RTW_YS_AHEAD
 #define RTW_YS_AHEAD 4
 #endif
+#ifndef RTW_YS_PACK
+#define RTW_YS_PACK 1  // the prefilter on packed fp32 pairs (rtw_scene_upload lays the records out for it)
+#endif
 constexpr int kYsAhead = RTW_YS_AHEAD;  // fp32 records in flight ahead of the filtered one
 RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, double fc) {
     const double a = dot(r.d, r.d);
@@ -659,6 +662,78 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
     // software-pipelined scalar loads of the fp32 records: the records of
     // the next kYsAhead spheres are in flight while sphere i is filtered (a
     // ring of registers, the loop unrolled by its length)
+    // the reference's test, sphere.h:46-81 (exact fp64), for a sphere the
+    // prefilter could not exclude
+    auto exact = [&](int i) {
+        const double* p = S.prims[first + i].p;
+        const d3 oc{r.o.x - ld(p), r.o.y - (ld(p + 1) + ld(p + 5) * fc), r.o.z - ld(p + 2)};
+        const double b = dot(oc, r.d);
+        const double c = dot(oc, oc) - ld(p + 9);
+        const double disc = b * b - a * c;
+        if (disc > 0) {
+            const double sq = __builtin_sqrt(disc);
+            double temp = walk_quot(-b - sq, a, ya, oka);
+            bool ok = temp < h.t && temp > t_min;
+            if (!ok) {
+                temp = walk_quot(-b + sq, a, ya, oka);
+                ok = temp < h.t && temp > t_min;
+            }
+            if (ok) {
+                h.t = temp;
+                h.prim = first + i;
+                h.rect = false;
+            }
+        }
+    };
+#if RTW_YS_PACK
+    // Two spheres per instruction: gfx950's packed fp32 VALU ops (v_pk_fma /
+    // v_pk_mul / v_pk_add_f32) run the filter of spheres 2p and 2p + 1
+    // side by side -- the same IEEE fp32 operations per sphere as the scalar
+    // form, so the bound above holds unchanged.  The upload interleaves the
+    // records of a run pairwise ({cx, cx', cy, cy', cz, cz', dy, dy', rr,
+    // rr'}), so one scalar load brings each pair's operands in adjacent
+    // registers.  The exact tests still run in list order (2p, then 2p + 1).
+    // A run of odd length ends with one sphere in the plain record, filtered
+    // alone.  (Runs hold at least two spheres: np >= 1.)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    struct ysrec2 {
+        f2 cx, cy, cz, dy, rr;
+    };
+    const int np = n >> 1;
+    auto load2 = [&](int p) {
+        const f2* g = reinterpret_cast<const f2*>(S.ysph + 8 * (size_t)(first + 2 * (p < np ? p : np - 1)));
+        return ysrec2{ld(g), ld(g + 1), ld(g + 2), ld(g + 3), ld(g + 4)};
+    };
+    const f2 ox2 = oxf, oy2 = oyf, oz2 = ozf, dx2 = dxf, dy2 = dyf, dz2 = dzf, fc2 = fcf, af2 = af;
+    constexpr int kAhead2 = (kYsAhead + 1) / 2;  // pairs in flight
+    ysrec2 ring2[kAhead2];
+#pragma unroll
+    for (int j = 0; j < kAhead2; ++j) ring2[j] = load2(j);
+    for (int p0 = 0; p0 < np; p0 += kAhead2) {
+#pragma unroll
+        for (int j = 0; j < kAhead2; ++j) {
+            const int p = p0 + j;
+            if (p >= np) break;
+            const ysrec2 cur = ring2[j];
+            ring2[j] = load2(p + kAhead2);
+            const f2 ocx = ox2 - cur.cx, ocy = oy2 - __builtin_elementwise_fma(cur.dy, fc2, cur.cy), ocz = oz2 - cur.cz;
+            const f2 b32 = __builtin_elementwise_fma(ocx, dx2, __builtin_elementwise_fma(ocy, dy2, ocz * dz2));
+            const f2 q32 = __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz));
+            const f2 d32 = __builtin_elementwise_fma(b32, b32, -(af2 * (q32 - cur.rr)));
+            const int i = 2 * p;
+            if (__builtin_amdgcn_ballot_w64(!(d32.x <= -E))) exact(i);
+            if (__builtin_amdgcn_ballot_w64(!(d32.y <= -E))) exact(i + 1);
+        }
+    }
+    if (n & 1) {
+        const float* g = S.ysph + 8 * (size_t)(first + n - 1);
+        const float ocx = oxf - ld(g), ocy = oyf - __builtin_fmaf(ld(g + 3), fcf, ld(g + 1)), ocz = ozf - ld(g + 2);
+        const float b32 = __builtin_fmaf(ocx, dxf, __builtin_fmaf(ocy, dyf, ocz * dzf));
+        const float q32 = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
+        const float d32 = __builtin_fmaf(b32, b32, -(af * (q32 - ld(g + 4))));
+        if (__builtin_amdgcn_ballot_w64(!(d32 <= -E))) exact(n - 1);
+    }
+#else
     struct ysrec {
         float cx, cy, cz, dy, rr;
     };
@@ -680,30 +755,10 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
             const float b32 = __builtin_fmaf(ocx, dxf, __builtin_fmaf(ocy, dyf, ocz * dzf));
             const float q32 = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
             const float d32 = __builtin_fmaf(b32, b32, -(af * (q32 - cur.rr)));
-            if (__builtin_amdgcn_ballot_w64(!(d32 <= -E))) {
-                // the reference's test, sphere.h:46-81 (exact fp64)
-                const double* p = S.prims[first + i].p;
-                const d3 oc{r.o.x - ld(p), r.o.y - (ld(p + 1) + ld(p + 5) * fc), r.o.z - ld(p + 2)};
-                const double b = dot(oc, r.d);
-                const double c = dot(oc, oc) - ld(p + 9);
-                const double disc = b * b - a * c;
-                if (disc > 0) {
-                    const double sq = __builtin_sqrt(disc);
-                    double temp = walk_quot(-b - sq, a, ya, oka);
-                    bool ok = temp < h.t && temp > t_min;
-                    if (!ok) {
-                        temp = walk_quot(-b + sq, a, ya, oka);
-                        ok = temp < h.t && temp > t_min;
-                    }
-                    if (ok) {
-                        h.t = temp;
-                        h.prim = first + i;
-                        h.rect = false;
-                    }
-                }
-            }
+            if (__builtin_amdgcn_ballot_w64(!(d32 <= -E))) exact(i);
         }
     }
+#endif
 }
 
 // Tie-exact test of prim `pi` against the running best, valid for ANY

@@ -1445,6 +1445,11 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     // within 2^4 are filtered, others (the random_balls ground, r = 1000)
     // carry r^2 = +inf and always take the fp64 test; the maxima over the
     // filtered ones bound the prefilter's rounding error
+    // (RTW_YS_PACK: the records of a run are interleaved pairwise, spheres
+    // first + 2p and first + 2p + 1 sharing the 16 floats at 8 (first + 2p),
+    // component c of member s at 2c + s; the last sphere of a run of odd
+    // length keeps the plain record {cx, cy, cz, dy, rr} in its own 8 floats,
+    // so every record stays inside its run's slots)
     std::vector<float> ysph(8 * std::max<size_t>(dprims.size(), 1), 0.0f);
     float ysb[5] = {0, 0, 0, 0, 0};  // |cx|, |cy|, |dy|, |cz|, r^2 maxima
     auto up = [](double v) {  // fp32 value >= v
@@ -1456,16 +1461,24 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         if (R.entry != WORLD_RUN_YSPHERES) continue;
         for (int i = R.first_prim; i < R.first_prim + R.n_prims; ++i) {
             const rtw_prim& q = dprims[i];
-            float* f = ysph.data() + 8 * (size_t)i;
+#if RTW_YS_PACK
+            const int k = i - R.first_prim;
+            const bool lone = k == R.n_prims - 1 && (k & 1) == 0;
+            float* const rec = ysph.data() + 8 * (size_t)(R.first_prim + (k & ~1)) + (k & 1);
+            auto f = [rec, lone](int c) -> float& { return rec[lone ? c : 2 * c]; };
+#else
+            float* const rec = ysph.data() + 8 * (size_t)i;
+            auto f = [rec](int c) -> float& { return rec[c]; };
+#endif
             const double dy = q.type == DP_MOVING_COMMON_Y ? q.p[5] : 0.0;
-            f[0] = (float)q.p[0], f[1] = (float)q.p[1], f[2] = (float)q.p[2], f[3] = (float)dy;
+            f(0) = (float)q.p[0], f(1) = (float)q.p[1], f(2) = (float)q.p[2], f(3) = (float)dy;
             const bool small = std::fabs(q.p[0]) <= 256 && std::fabs(q.p[1]) <= 256 && std::fabs(dy) <= 256 &&
                                std::fabs(q.p[2]) <= 256 && std::fabs(q.p[3]) <= 16;
             if (!small) {
-                f[4] = INFINITY;
+                f(4) = INFINITY;
                 continue;
             }
-            f[4] = (float)q.p[9];
+            f(4) = (float)q.p[9];
             ysb[0] = std::max(ysb[0], up(std::fabs(q.p[0])));
             ysb[1] = std::max(ysb[1], up(std::fabs(q.p[1])));
             ysb[2] = std::max(ysb[2], up(std::fabs(dy)));
