@@ -91,6 +91,9 @@ public:
         for (int k = 0; k < 6; ++k)
             Add(mover(vec3(-2.5 + k, 0.3, 1.5), vec3(-2.5 + k, 0.3 + 0.1 * k, 1.5), 0.3, k & 1 ? red : white, 0.0, 1.0));
         Add(std::make_shared<sphere>(vec3(1.7, 0.4, -0.6), 0.4, glass));
+        // a ninth sphere: the run's length is odd, so ysphere_scan's packed
+        // pairs end with a lone sphere filtered from its plain record
+        Add(std::make_shared<sphere>(vec3(-1.2, 0.2, 0.6), 0.2, red));
         // a light between the runs: translated (by zero, which moves nothing)
         // so that it is not a plain entry -- a flip alone folds into the prim
         // and would merge run 1, the lamp and run 2 into one mixed run
