@@ -680,7 +680,6 @@ void k_persist(persist_args) {
     }
     if (LDS || LST) __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
-    ray_batch& B = s_batch[threadIdx.x >> 6];
     const int own = blockIdx.x % kQShards;
     path_st x;
     x.depth = 0;
@@ -696,6 +695,9 @@ void k_persist(persist_args) {
         uint32_t tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         const uint32_t ln = tid & 63;
+        // (the wave's batch too: formed once per kernel, its per-array
+        // addresses were held in 15 VGPRs across the whole loop)
+        ray_batch& B = s_batch[tid >> 6];
         for (int round = 0; round < 2; ++round) {
             const unsigned long long m = __ballot(x.depth == 0);
             if (!m) break;
