@@ -700,8 +700,12 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
         f2 cx, cy, cz, dy, rr;
     };
     const int np = n >> 1;
+    // (the prefetch runs past the run's last pair into the records that
+    // follow -- the upload pads the array for it -- and those are never
+    // used: no clamp, so each load is the run's base plus a constant offset)
+    const f2* const g0 = reinterpret_cast<const f2*>(S.ysph + 8 * (size_t)first);
     auto load2 = [&](int p) {
-        const f2* g = reinterpret_cast<const f2*>(S.ysph + 8 * (size_t)(first + 2 * (p < np ? p : np - 1)));
+        const f2* g = g0 + 8 * p;
         return ysrec2{ld(g), ld(g + 1), ld(g + 2), ld(g + 3), ld(g + 4)};
     };
     const f2 ox2 = oxf, oy2 = oyf, oz2 = ozf, dx2 = dxf, dy2 = dyf, dz2 = dzf, fc2 = fcf, af2 = af;

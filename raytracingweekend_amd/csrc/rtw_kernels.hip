@@ -1451,8 +1451,9 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     // first + 2p and first + 2p + 1 sharing the 16 floats at 8 (first + 2p),
     // component c of member s at 2c + s; the last sphere of a run of odd
     // length keeps the plain record {cx, cy, cz, dy, rr} in its own 8 floats,
-    // so every record stays inside its run's slots)
-    std::vector<float> ysph(8 * std::max<size_t>(dprims.size(), 1), 0.0f);
+    // so every record stays inside its run's slots; kYsAhead + 2 spare
+    // records at the end for the prefetch that runs past a run's last pair)
+    std::vector<float> ysph(8 * (std::max<size_t>(dprims.size(), 1) + kYsAhead + 2), 0.0f);
     float ysb[5] = {0, 0, 0, 0, 0};  // |cx|, |cy|, |dy|, |cz|, r^2 maxima
     auto up = [](double v) {  // fp32 value >= v
         float f = (float)v;
