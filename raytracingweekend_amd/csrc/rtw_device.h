@@ -720,7 +720,13 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
             if (p >= np) break;
             const ysrec2 cur = ring2[j];
             ring2[j] = load2(p + kAhead2);
-            const f2 ocx = ox2 - cur.cx, ocy = oy2 - __builtin_elementwise_fma(cur.dy, fc2, cur.cy), ocz = oz2 - cur.cz;
+            // ocy as (oy - cy) - dy fc: each instruction then reads one
+            // scalar pair (one SGPR operand per VALU instruction), where
+            // oy - (dy fc + cy) needed cy copied to vector registers first;
+            // two roundings either way, within the same 2u (|oy| + |cy| +
+            // |dy fc|) the bound above allows for
+            const f2 ocx = ox2 - cur.cx, ocz = oz2 - cur.cz;
+            const f2 ocy = __builtin_elementwise_fma(-cur.dy, fc2, oy2 - cur.cy);
             const f2 b32 = __builtin_elementwise_fma(ocx, dx2, __builtin_elementwise_fma(ocy, dy2, ocz * dz2));
             const f2 q32 = __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz));
             const f2 d32 = __builtin_elementwise_fma(b32, b32, -(af2 * (q32 - cur.rr)));
