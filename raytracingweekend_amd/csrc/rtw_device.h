@@ -700,40 +700,44 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
         f2 cx, cy, cz, dy, rr;
     };
     const int np = n >> 1;
-    // (the prefetch runs past the run's last pair into the records that
-    // follow -- the upload pads the array for it -- and those are never
-    // used: no clamp, so each load is the run's base plus a constant offset)
+    // (each load is the run's base plus a constant offset: no index clamp,
+    // every pair read lies inside the run)
     const f2* const g0 = reinterpret_cast<const f2*>(S.ysph + 8 * (size_t)first);
     auto load2 = [&](int p) {
         const f2* g = g0 + 8 * p;
         return ysrec2{ld(g), ld(g + 1), ld(g + 2), ld(g + 3), ld(g + 4)};
     };
     const f2 ox2 = oxf, oy2 = oyf, oz2 = ozf, dx2 = dxf, dy2 = dyf, dz2 = dzf, fc2 = fcf, af2 = af;
-    constexpr int kAhead2 = (kYsAhead + 1) / 2;  // pairs in flight
-    ysrec2 ring2[kAhead2];
-#pragma unroll
-    for (int j = 0; j < kAhead2; ++j) ring2[j] = load2(j);
-    for (int p0 = 0; p0 < np; p0 += kAhead2) {
-#pragma unroll
-        for (int j = 0; j < kAhead2; ++j) {
-            const int p = p0 + j;
-            if (p >= np) break;
-            const ysrec2 cur = ring2[j];
-            ring2[j] = load2(p + kAhead2);
-            // ocy as (oy - cy) - dy fc: each instruction then reads one
-            // scalar pair (one SGPR operand per VALU instruction), where
-            // oy - (dy fc + cy) needed cy copied to vector registers first;
-            // two roundings either way, within the same 2u (|oy| + |cy| +
-            // |dy fc|) the bound above allows for
-            const f2 ocx = ox2 - cur.cx, ocz = oz2 - cur.cz;
-            const f2 ocy = __builtin_elementwise_fma(-cur.dy, fc2, oy2 - cur.cy);
-            const f2 b32 = __builtin_elementwise_fma(ocx, dx2, __builtin_elementwise_fma(ocy, dy2, ocz * dz2));
-            const f2 q32 = __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz));
-            const f2 d32 = __builtin_elementwise_fma(b32, b32, -(af2 * (q32 - cur.rr)));
-            const int i = 2 * p;
-            if (__builtin_amdgcn_ballot_w64(!(d32.x <= -E))) exact(i);
-            if (__builtin_amdgcn_ballot_w64(!(d32.y <= -E))) exact(i + 1);
-        }
+    // ocy as (oy - cy) - dy fc: each instruction then reads one scalar pair
+    // (one SGPR operand per VALU instruction), where oy - (dy fc + cy)
+    // needed cy copied to vector registers first; two roundings either way,
+    // within the same 2u (|oy| + |cy| + |dy fc|) the bound above allows for
+    auto filt = [&](const ysrec2& c) {
+        const f2 ocx = ox2 - c.cx, ocz = oz2 - c.cz;
+        const f2 ocy = __builtin_elementwise_fma(-c.dy, fc2, oy2 - c.cy);
+        const f2 b32 = __builtin_elementwise_fma(ocx, dx2, __builtin_elementwise_fma(ocy, dy2, ocz * dz2));
+        const f2 q32 = __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz));
+        return __builtin_elementwise_fma(b32, b32, -(af2 * (q32 - c.rr)));
+    };
+    // two pairs per iteration: both filters first (independent chains the
+    // scheduler interleaves, so no hazard stalls between dependent packed
+    // instructions), then the exact tests in list order
+    int p = 0;
+    for (; p + 2 <= np; p += 2) {
+        const f2 d0 = filt(load2(p)), d1 = filt(load2(p + 1));
+        const unsigned long long m0 = __builtin_amdgcn_ballot_w64(!(d0.x <= -E));
+        const unsigned long long m1 = __builtin_amdgcn_ballot_w64(!(d0.y <= -E));
+        const unsigned long long m2 = __builtin_amdgcn_ballot_w64(!(d1.x <= -E));
+        const unsigned long long m3 = __builtin_amdgcn_ballot_w64(!(d1.y <= -E));
+        if (m0) exact(2 * p);
+        if (m1) exact(2 * p + 1);
+        if (m2) exact(2 * p + 2);
+        if (m3) exact(2 * p + 3);
+    }
+    if (p < np) {
+        const f2 d0 = filt(load2(p));
+        if (__builtin_amdgcn_ballot_w64(!(d0.x <= -E))) exact(2 * p);
+        if (__builtin_amdgcn_ballot_w64(!(d0.y <= -E))) exact(2 * p + 1);
     }
     if (n & 1) {
         const float* g = S.ysph + 8 * (size_t)(first + n - 1);

@@ -1452,7 +1452,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     // component c of member s at 2c + s; the last sphere of a run of odd
     // length keeps the plain record {cx, cy, cz, dy, rr} in its own 8 floats,
     // so every record stays inside its run's slots; kYsAhead + 2 spare
-    // records at the end for the prefetch that runs past a run's last pair)
+    // records at the end, slack for the unpacked form's prefetch ring)
     std::vector<float> ysph(8 * (std::max<size_t>(dprims.size(), 1) + kYsAhead + 2), 0.0f);
     float ysb[5] = {0, 0, 0, 0, 0};  // |cx|, |cy|, |dy|, |cz|, r^2 maxima
     auto up = [](double v) {  // fp32 value >= v
