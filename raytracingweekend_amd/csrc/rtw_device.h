@@ -635,6 +635,10 @@ RTW_D double walk_quot(double num, double den, double y, bool ok) {
 #ifndef RTW_YS_AHEAD
 #define RTW_YS_AHEAD 4
 #endif
+#ifndef RTW_YS_GROUP
+#define RTW_YS_GROUP 4  // packed pairs filtered together per iteration (2: -1.7 %, 3: -2.5 %)
+#endif
+constexpr int kYsGroup = RTW_YS_GROUP;
 #ifndef RTW_YS_PACK
 #define RTW_YS_PACK 1  // the prefilter on packed fp32 pairs (rtw_scene_upload lays the records out for it)
 #endif
@@ -719,22 +723,26 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
         const f2 q32 = __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz));
         return __builtin_elementwise_fma(b32, b32, -(af2 * (q32 - c.rr)));
     };
-    // two pairs per iteration: both filters first (independent chains the
-    // scheduler interleaves, so no hazard stalls between dependent packed
-    // instructions), then the exact tests in list order
+    // kYsGroup pairs per iteration: all their filters first (independent
+    // chains the scheduler interleaves, so no hazard stalls between
+    // dependent packed instructions), then the ballots, then the exact tests
+    // in list order
     int p = 0;
-    for (; p + 2 <= np; p += 2) {
-        const f2 d0 = filt(load2(p)), d1 = filt(load2(p + 1));
-        const unsigned long long m0 = __builtin_amdgcn_ballot_w64(!(d0.x <= -E));
-        const unsigned long long m1 = __builtin_amdgcn_ballot_w64(!(d0.y <= -E));
-        const unsigned long long m2 = __builtin_amdgcn_ballot_w64(!(d1.x <= -E));
-        const unsigned long long m3 = __builtin_amdgcn_ballot_w64(!(d1.y <= -E));
-        if (m0) exact(2 * p);
-        if (m1) exact(2 * p + 1);
-        if (m2) exact(2 * p + 2);
-        if (m3) exact(2 * p + 3);
+    for (; p + kYsGroup <= np; p += kYsGroup) {
+        f2 d[kYsGroup];
+#pragma unroll
+        for (int j = 0; j < kYsGroup; ++j) d[j] = filt(load2(p + j));
+        unsigned long long m[2 * kYsGroup];
+#pragma unroll
+        for (int j = 0; j < kYsGroup; ++j) {
+            m[2 * j] = __builtin_amdgcn_ballot_w64(!(d[j].x <= -E));
+            m[2 * j + 1] = __builtin_amdgcn_ballot_w64(!(d[j].y <= -E));
+        }
+#pragma unroll
+        for (int k = 0; k < 2 * kYsGroup; ++k)
+            if (m[k]) exact(2 * p + k);
     }
-    if (p < np) {
+    for (; p < np; ++p) {
         const f2 d0 = filt(load2(p));
         if (__builtin_amdgcn_ballot_w64(!(d0.x <= -E))) exact(2 * p);
         if (__builtin_amdgcn_ballot_w64(!(d0.y <= -E))) exact(2 * p + 1);
