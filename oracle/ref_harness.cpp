@@ -26,7 +26,8 @@
 //   scene  <name> <aspect>                  JSON dump of the scene graph
 //   render <name> <nx> <ny> <spp> <depth> <seed> <threads> <out.bin>
 //          writes nx*ny*3 doubles: per-pixel radiance SUM over spp samples
-//   bench  <name> <nx> <ny> <spp> <depth> <seed> <threads>
+//   bench  <name> <nx> <ny> <spp> <depth> <seed> <threads> [row_stride]
+//          times render() over every row_stride-th row (default: all rows)
 //   perlin                                  Perlin tables + noise/turb samples
 #include "rng_inject.h"
 
@@ -282,15 +283,17 @@ static void init_perlin() {
 
 // Render loop body of RayTracingWeekend.cpp:214-241 (without the gamma step,
 // which the tests apply to the returned sums exactly as :241-244 does).
+// row_stride > 1 renders rows 0, row_stride, 2*row_stride, ... only (a bounded
+// sample of a large image for the bench's CPU baseline); other rows stay 0.
 static void render(scene* sc, int nx, int ny, int spp, int depth, uint64_t seed, int threads,
-                   std::vector<double>& sums, uint64_t& segments) {
+                   std::vector<double>& sums, uint64_t& segments, int row_stride = 1) {
     init_perlin();
     camera& cam = sc->GetCamera();
     sums.assign((size_t)nx * ny * 3, 0.0);
     uint64_t seg_total = 0;
     omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : seg_total)
-    for (int j = 0; j < ny; j++) {
+    for (int j = 0; j < ny; j += row_stride) {
         g_segments = 0;
         std::uniform_real_distribution<double> uniform;
         std::minstd_rand engine;  // -> per-path stream while a key is active
@@ -520,19 +523,21 @@ int main(int argc, char** argv) {
         dump_perlin();
         return 0;
     }
-    if ((cmd == "render" && argc == 10) || (cmd == "bench" && argc == 9) || (cmd == "ppm" && argc == 10)) {
+    if ((cmd == "render" && argc == 10) || (cmd == "bench" && (argc == 9 || argc == 10)) ||
+        (cmd == "ppm" && argc == 10)) {
         std::string name = argv[2];
         int nx = atoi(argv[3]), ny = atoi(argv[4]), spp = atoi(argv[5]), depth = atoi(argv[6]);
         uint64_t seed = strtoull(argv[7], nullptr, 10);
         int threads = atoi(argv[8]);
+        int row_stride = (cmd == "bench" && argc == 10) ? std::max(1, atoi(argv[9])) : 1;
         scene* sc = make_scene(name, nx * 1.0 / ny);  // RayTracingWeekend.cpp:204
         std::vector<double> sums;
         uint64_t segments = 0;
         auto t0 = std::chrono::steady_clock::now();
-        render(sc, nx, ny, spp, depth, seed, threads, sums, segments);
+        render(sc, nx, ny, spp, depth, seed, threads, sums, segments, row_stride);
         auto t1 = std::chrono::steady_clock::now();
         double sec = std::chrono::duration<double>(t1 - t0).count();
-        double samples = (double)nx * ny * spp;
+        double samples = (double)nx * ((ny + row_stride - 1) / row_stride) * spp;
         printf("{\"seconds\":%.6f,\"samples\":%.0f,\"segments\":%llu,\"msamples_per_s\":%.6f,\"threads\":%d}\n", sec,
                samples, (unsigned long long)segments, samples / sec / 1e6, threads);
         if (cmd == "ppm") return write_ppm_reference(argv[9], sums, nx, ny, spp);
