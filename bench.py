@@ -48,6 +48,8 @@ METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"] if (ROOT / "
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # fp64 VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction
 VALU_PEAK_GINST = 1024 * 2.4 / 4
+# VALU issue cycles available: 1024 SIMDs x 2.4 GHz
+VALU_SIMD_GCYC = 1024 * 2.4
 PMC_DIR = ROOT / "profiles" / "pmc"
 
 # BASELINE.json configs; spp is the image's TOTAL samples per pixel
@@ -199,14 +201,31 @@ def roofline(args, kernel, build, seg, ms, launches, algo):
     traffic = round(rec["hbm_bytes_per_launch"] * scale, 1)
     hbm["traffic"] = traffic
     ipw = rec["valu_insts_per_wave_segment"]
-    ach = ipw * seg_launch / 64 / (avg_ms * 1e-3) / 1e9
-    out.update({"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
-                "frac": round(ach / VALU_PEAK_GINST, 4), "traffic": traffic,
-                "valu_insts_per_wave_segment": round(ipw, 1), "pmc": src,
-                "definition": "VALU wave-instructions per traversal (SQ_INSTS_VALU of the PMC record of this "
-                              "kernel, build and workload) x device-counted traversals / HIP-event launch time, "
-                              "against 1 wave64 VALU instruction per 4 cycles per SIMD at 2.4 GHz",
-                "hbm": hbm})
+    issue = ipw * seg_launch / 64 / (avg_ms * 1e-3) / 1e9
+    out.update({"traffic": traffic, "valu_insts_per_wave_segment": round(ipw, 1), "pmc": src, "hbm": hbm,
+                "issue_model": {"achieved": round(issue, 1), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
+                                "frac": round(issue / VALU_PEAK_GINST, 4),
+                                "definition": "VALU wave-instructions (SQ_INSTS_VALU) x traversals / launch time, "
+                                              "every instruction priced at the fp64 rate (4 cycles per SIMD)"}})
+    busy = rec.get("valu_busy_cycles_per_segment")
+    if busy:
+        # measured: the cycles the SIMDs spent issuing VALU instructions
+        # (4 x SQ_ACTIVE_INST_VALU per traversal of the record) x this run's
+        # traversals / its HIP-event launch time, against every SIMD busy
+        ach = busy * seg_launch / (avg_ms * 1e-3) / 1e9
+        lane = rec.get("valu_lane_util")
+        out.update({"bound": "valu", "achieved": round(ach, 1), "peak": VALU_SIMD_GCYC, "unit": "G SIMD-cycles/s",
+                    "frac": round(ach / VALU_SIMD_GCYC, 4),
+                    "valu_lane_util": round(lane, 4) if lane else None,
+                    "valu_useful_frac": round(ach / VALU_SIMD_GCYC * lane, 4) if lane else None,
+                    "definition": "VALU-busy SIMD cycles per traversal (4 x SQ_ACTIVE_INST_VALU of the PMC record of "
+                                  "this kernel, build and workload) x device-counted traversals / HIP-event launch "
+                                  "time, against 1024 SIMDs x 2.4 GHz; valu_lane_util = SQ_THREAD_CYCLES_VALU / (64 x "
+                                  "SQ_ACTIVE_INST_VALU), the share of lanes doing work in those cycles"})
+    else:
+        out.update({"bound": "valu", "achieved": round(issue, 1), "peak": VALU_PEAK_GINST,
+                    "unit": "G wave-instr/s", "frac": round(issue / VALU_PEAK_GINST, 4),
+                    "definition": out["issue_model"]["definition"]})
     return out
 
 

@@ -39,10 +39,10 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 2
-#ifndef RTW_MAX_OPS
+#define RTW_ABI_VERSION 3
+/* Fixed by the ABI: it sizes rtw_entry (op / op_param).  A client built with
+ * another value would lay entries out differently from this library. */
 #define RTW_MAX_OPS 8
-#endif
 
 /* ------------------------------------------------------------------ */
 /* status codes                                                        */
@@ -238,8 +238,16 @@ typedef struct rtw_render_params {
     int32_t collect_kernel_times; /* 1: hipEvents around traversal launches,    */
                                   /* 2: and shade launches (adds queue gaps)   */
     int32_t wavefront_paths; /* paths in flight (0 = library default)             */
-    int32_t reserved;
+    int32_t precision;     /* rtw_precision: RTW_PRECISION_FP64 (0) = the reference's
+                              double arithmetic, parity with the CPU renderer;
+                              RTW_PRECISION_FP32 (1) = fast mode, single precision
+                              traversal and shading, statistical parity only     */
 } rtw_render_params;
+
+typedef enum rtw_precision {
+    RTW_PRECISION_FP64 = 0,
+    RTW_PRECISION_FP32 = 1
+} rtw_precision;
 
 typedef struct rtw_stats {
     uint64_t samples;        /* camera samples completed                          */

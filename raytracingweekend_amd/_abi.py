@@ -13,7 +13,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("RTW_LIBRARY", PKG / "librtw.so"))
 
-RTW_ABI_VERSION = 2
+RTW_ABI_VERSION = 3
 RTW_MAX_OPS = 8
 
 # enums (rtw_gpu.h)
@@ -25,6 +25,8 @@ RTW_TEX_CONSTANT, RTW_TEX_CHECKER, RTW_TEX_NOISE = range(3)
 RTW_LIGHT_DEFAULT, RTW_LIGHT_XZ_RECT, RTW_LIGHT_SPHERE = range(3)
 RTW_RENDER_SHADED, RTW_RENDER_NORMAL = 0, 1
 RTW_BG_BLACK, RTW_BG_GRADIENT = 0, 1
+RTW_PRECISION_FP64, RTW_PRECISION_FP32 = 0, 1
+PRECISIONS = {"fp64": RTW_PRECISION_FP64, "fp32": RTW_PRECISION_FP32}
 
 
 class rtw_prim(C.Structure):
@@ -81,7 +83,7 @@ class rtw_render_params(C.Structure):
     _fields_ = [("nx", C.c_int32), ("ny", C.c_int32), ("spp", C.c_int32), ("max_depth", C.c_int32),
                 ("seed", C.c_uint64), ("spp_begin", C.c_int32), ("spp_count", C.c_int32),
                 ("row_begin", C.c_int32), ("row_step", C.c_int32), ("accum_on_device", C.c_int32),
-                ("collect_kernel_times", C.c_int32), ("wavefront_paths", C.c_int32), ("reserved", C.c_int32)]
+                ("collect_kernel_times", C.c_int32), ("wavefront_paths", C.c_int32), ("precision", C.c_int32)]
 
 
 class rtw_stats(C.Structure):

@@ -454,6 +454,14 @@ struct flattener {
             }
             if (!flatten_node(k, inner, seq, m)) return false;
         }
+        if (m && dynamic_cast<const bvh_node*>(body)) {
+            // the reference's bvh_node::hit walks `left` twice and never
+            // `right` (hittable.h:82-110): there is no walk order whose media
+            // draws could be reproduced, so refuse rather than guess
+            err = "a bvh_node holding a constant_medium is unsupported (the reference's bvh_node::hit is broken, "
+                  "hittable.h:82-110)";
+            return false;
+        }
         out.insert(out.end(), seq.begin(), seq.end());
         if (m && is_list) {  // the list's second walk (hittable_list.h:26-34)
             for (int32_t v : seq) out.push_back(v | RTW_VISIT_REPLAY);

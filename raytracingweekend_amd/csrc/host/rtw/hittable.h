@@ -2,10 +2,13 @@
 //
 // The classes keep the reference's names, constructor signatures and public
 // fields, so scene code written against the reference compiles unchanged.
-// They describe geometry; closest-hit queries (hit / pdf_value / random) are
-// answered by the device kernels after rtw_flatten_scene() has turned the
-// graph into an rtw_scene_desc.  bounding_box() keeps the reference's results
-// (including the +-0.0001f rect slabs and rotate_y's rotated corner box).
+// They describe geometry; closest-hit queries (hit) are answered by the
+// device kernels after rtw_flatten_scene() has turned the graph into an
+// rtw_scene_desc.  bounding_box() keeps the reference's results (including
+// the +-0.0001f rect slabs and rotate_y's rotated corner box), and the light
+// sampling surface pdf_value() / random() (hittable.h:36-37, the xz_rect,
+// sphere and hittable_list overrides) is evaluated on the host with the
+// reference's arithmetic for pdf.h's hittable_pdf.
 #pragma once
 #include <cfloat>
 #include <cmath>
@@ -14,11 +17,16 @@
 #include <vector>
 #include "aabb.h"
 #include "material.h"
+#include "onb.h"
+#include "utility.h"
 
 class hittable {
 public:
     virtual ~hittable() {}
     virtual bool bounding_box(double t0, double t1, aabb& box) const = 0;
+    // hittable.h:36-37: the defaults for objects that are not light shapes
+    virtual double pdf_value(const vec3& o, const vec3& v) const { return 0.0; }
+    virtual vec3 random(const vec3& o) const { return vec3(1, 0, 0); }
 };
 
 class xy_rect : public hittable {
@@ -42,6 +50,27 @@ public:
     bool bounding_box(double, double, aabb& box) const override {
         box = aabb(vec3(x0, k - 0.0001f, z0), vec3(x1, k + 0.0001f, z1));
         return true;
+    }
+    // hittable.h:208-222: the solid-angle density of a hit of the rect along
+    // v, through xz_rect::hit (:184-200) on a ray of time FLT_MAX, t in
+    // (0.001, +inf]
+    double pdf_value(const vec3& origin, const vec3& v) const override {
+        const ray r(origin, v, FLT_MAX);
+        const double t = (k - r.origin().y) / r.direction().y;
+        if (t < 0.001 || t > std::numeric_limits<double>::infinity()) return 0;
+        const double x = r.origin().x + t * r.direction().x;
+        const double z = r.origin().z + t * r.direction().z;
+        if (x < x0 || x > x1 || z < z0 || z > z1) return 0;
+        const double area = (x1 - x0) * (z1 - z0);
+        const double distance_squared = t * t * v.length_squared();
+        const double cosine = std::fabs(dot(v, vec3(0, 1, 0)) / v.length());
+        return distance_squared / (cosine * area);
+    }
+    // hittable.h:224-228 (z drawn first, as g++ evaluates the vec3 arguments)
+    vec3 random(const vec3& origin) const override {
+        const double rz = random_double(z0, z1);
+        const double rx = random_double(x0, x1);
+        return vec3(rx, k, rz) - origin;
     }
     double x0, x1, z0, z1, k;
     std::shared_ptr<material> mp;

@@ -8,6 +8,18 @@ public:
     hittable_list(const std::vector<std::shared_ptr<hittable>>& l) : objects(l) {}
     // As the reference (hittable_list.h:39-42): reports true without setting `box`.
     bool bounding_box(double, double, aabb&) const override { return true; }
+    // hittable_list.h:44-53: the members' densities, equally weighted
+    double pdf_value(const vec3& o, const vec3& v) const override {
+        const double weight = 1.0 / objects.size();
+        double sum = 0.0;
+        for (const auto& object : objects) sum += weight * object->pdf_value(o, v);
+        return sum;
+    }
+    // hittable_list.h:55-59: a uniformly chosen member's direction
+    vec3 random(const vec3& o) const override {
+        const int int_size = static_cast<int>(objects.size());
+        return objects[random_int(0, int_size - 1)]->random(o);
+    }
     std::vector<std::shared_ptr<hittable>> objects;
 };
 

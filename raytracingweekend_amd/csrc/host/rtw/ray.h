@@ -1,8 +1,5 @@
-// ray.h / aabb.h surface of the host scene API (reference: ray.h:5-21,
-// aabb.h:10-65).  aabb::hit is kept for API compatibility and host-side tests
-// of the reference's slab semantics (std::max/std::min, reject tmax <= tmin).
+// ray.h surface of the host scene API (reference ray.h:5-21).
 #pragma once
-#include <utility>
 #include "vec3.h"
 
 class ray {
@@ -18,31 +15,4 @@ private:
     vec3 o_, d_;
     double t_ = 0.0;
 };
-
-class aabb {
-public:
-    aabb() {}
-    aabb(const vec3& lo, const vec3& hi) : _min(lo), _max(hi) {}
-    vec3 min() const { return _min; }
-    vec3 max() const { return _max; }
-
-    bool hit(const ray& r, double tmin, double tmax) const {
-        for (int a = 0; a < 3; ++a) {
-            const double inv = 1.0 / r.direction()[a];
-            double ta = (_min[a] - r.origin()[a]) * inv;
-            double tb = (_max[a] - r.origin()[a]) * inv;
-            if (inv < 0.0) std::swap(ta, tb);
-            tmin = std::max(ta, tmin);
-            tmax = std::min(tb, tmax);
-            if (tmax <= tmin) return false;
-        }
-        return true;
-    }
-
-    static aabb surrounding(const aabb& p, const aabb& q) {
-        return aabb(vec3(std::fmin(p._min.x, q._min.x), std::fmin(p._min.y, q._min.y), std::fmin(p._min.z, q._min.z)),
-                    vec3(std::fmax(p._max.x, q._max.x), std::fmax(p._max.y, q._max.y), std::fmax(p._max.z, q._max.z)));
-    }
-
-    vec3 _min, _max;
-};
+#include "aabb.h"  // scene code reaches aabb through the ray / hittable headers

@@ -22,3 +22,7 @@ T* rtw_dup(const std::vector<T>& v) {
 // the host library (multi.cpp); not part of the C ABI.
 int rtw_handle_device(void* handle);                                             // -1 for null
 int rtw_handle_add_device(void* handle, double* dst, const double* src, size_t n);  // dst += src, synchronous
+// RTW_OK when `p` is device memory of `device` (an accum_on_device pointer),
+// else RTW_ERR_INVALID naming `what`: a foreign pointer would be written by
+// kernels of another GPU (a fault, or silent peer writes).
+int rtw_check_device_ptr(const void* p, int device, const char* what);

@@ -27,7 +27,10 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 #include "rtw_device.h"
 #include "host/rtw_host_util.h"
@@ -1786,33 +1789,39 @@ bool launch_segment(bool probe, int f, int mask, int grid, hipStream_t st, const
     return false;
 }
 
-// Persistent kernel for the same instantiation set.  grid 0 = probe only.
-// The grid is the number of blocks that can be resident at once (occupancy
-// query per instantiation, cached), so every block starts immediately.
+// Resident workgroups per CU of kernel `fn` at `block` threads and `shm`
+// bytes of dynamic LDS on the current device: one occupancy query per
+// (kernel, block, LDS bytes, device), cached.  rtw_render_multi renders from
+// one host thread per device at once, so the cache is guarded; a failed
+// query is not cached (2 blocks per CU is assumed for that launch).
+int blocks_per_cu(const void* fn, int block, size_t shm) {
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, int, size_t, int>, int> cache;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return 2;
+    const auto key = std::make_tuple(fn, block, shm, dev);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        const auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, block, shm) != hipSuccess || nb <= 0) return 2;
+    std::lock_guard<std::mutex> g(mu);
+    cache[key] = nb;
+    return nb;
+}
+
+// Persistent kernel for the same instantiation set.  The grid is the number
+// of blocks that can be resident at once, so every block starts immediately.
 template <int FF, int MM, bool LL, bool LST>
 int persist_grid(size_t shm, int cus) {
-    static int blocks_per_cu = 0;
-    if (!blocks_per_cu) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void*>(&k_persist<FF, MM, LL, LST>), kBlock, shm) != hipSuccess || nb <= 0)
-            nb = 2;
-        blocks_per_cu = nb;
-    }
-    return blocks_per_cu * cus;
+    return blocks_per_cu(reinterpret_cast<const void*>(&k_persist<FF, MM, LL, LST>), kBlock, shm) * cus;
 }
 
 template <int FF, int MM, bool LL>
 int persist_sort_grid(size_t shm, int cus) {
-    static int blocks_per_cu = 0;
-    if (!blocks_per_cu) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void*>(&k_persist_sort<FF, MM, LL>), kSortBlock, shm) != hipSuccess || nb <= 0)
-            nb = 2;
-        blocks_per_cu = nb;
-    }
-    return blocks_per_cu * cus;
+    return blocks_per_cu(reinterpret_cast<const void*>(&k_persist_sort<FF, MM, LL>), kSortBlock, shm) * cus;
 }
 
 // The persistent kernels: material-regrouping k_persist_sort for list
@@ -1841,16 +1850,12 @@ uint32_t node_packet(size_t shm, int n_nodes) {
     cap = std::min<uint32_t>(cap, (uint32_t)std::max(0, n_nodes));
     if (!cap) return 0;
     const void* fn = reinterpret_cast<const void*>(&k_persist<FF, MM, LL, true>);
-    int base = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&base, fn, kBlock, shm) != hipSuccess || base <= 0) return 0;
+    const int base = blocks_per_cu(fn, kBlock, shm);
     const size_t off = (shm + 15) & ~size_t(15);
     uint32_t best = 0;
     for (uint32_t k = 32; k <= cap + 31; k += 32) {
         const uint32_t kk = std::min(k, cap);
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kBlock, off + kk * sizeof(bvh_node32)) != hipSuccess ||
-            nb < base)
-            break;
+        if (blocks_per_cu(fn, kBlock, off + kk * sizeof(bvh_node32)) < base) break;
         best = kk;
         if (kk == cap) break;
     }
@@ -2213,6 +2218,21 @@ int rtw_handle_add_device(void* handle, double* dst, const double* src, size_t n
     return RTW_OK;
 }
 
+int rtw_check_device_ptr(const void* p, int device, const char* what) {
+    hipPointerAttribute_t a;
+    std::memset(&a, 0, sizeof a);
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeDevice) {
+        (void)hipGetLastError();  // clear the sticky error of a failed query
+        return rtw_fail(RTW_ERR_INVALID, std::string(what) + ": accum_on_device is set but the accumulator is not "
+                                                              "device memory");
+    }
+    if (a.device != device)
+        return rtw_fail(RTW_ERR_INVALID, std::string(what) + ": the device accumulator lives on device " +
+                                             std::to_string(a.device) + ", the scene on device " +
+                                             std::to_string(device));
+    return RTW_OK;
+}
+
 extern "C" int rtw_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -2296,6 +2316,8 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         return rtw_fail(RTW_ERR_INVALID, "rtw_render_accumulate: bad image / sample parameters");
     const int spp_count = R.spp_count ? R.spp_count : R.spp - R.spp_begin;
     if (R.spp_begin + (long long)spp_count > R.spp) return rtw_fail(RTW_ERR_INVALID, "sample range exceeds spp");
+    if (R.precision != RTW_PRECISION_FP64 && R.precision != RTW_PRECISION_FP32)
+        return rtw_fail(RTW_ERR_INVALID, "rtw_render_accumulate: unknown precision");
     const int row_step = R.row_step > 0 ? R.row_step : 1;
     if (R.row_begin < 0 || R.row_begin >= R.ny) return rtw_fail(RTW_ERR_INVALID, "row_begin out of range");
     const int n_rows = (R.ny - R.row_begin + row_step - 1) / row_step;
@@ -2308,6 +2330,8 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                         "rtw_render_accumulate: camera shutter outside the one the scene's BVH was built for "
                         "(moving spheres); flatten the scene with this camera");
     HIPCHK(hipSetDevice(h->device));
+    if (R.accum_on_device)
+        if (int rc = rtw_check_device_ptr(accum_rgb, h->device, "rtw_render_accumulate")) return rc;
     hipStream_t st = h->stream;
 
     rtw_stats stats;

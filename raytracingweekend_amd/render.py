@@ -65,10 +65,12 @@ class DeviceScene:
     def render_accumulate(self, nx: int, ny: int, spp: int, max_depth: int, seed: int = 0, *,
                           spp_begin: int = 0, spp_count: int = 0, row_begin: int = 0, row_step: int = 1,
                           accum=None, camera: Optional[_abi.rtw_camera_desc] = None,
-                          collect_kernel_times: bool = False, wavefront_paths: int = 0):
+                          collect_kernel_times: bool = False, wavefront_paths: int = 0, precision: str = "fp64"):
         """Add the per-pixel radiance sums of the selected samples into `accum`
         (a float64 numpy array of nx*ny*3, or a torch float64 CUDA tensor on
-        this device).  Returns (accum, stats dict)."""
+        this device).  precision "fp64" is the reference's arithmetic (parity
+        mode); "fp32" the fast mode (statistical parity only).  Returns
+        (accum, stats dict)."""
         if accum is None:
             accum = np.zeros(nx * ny * 3, dtype=np.float64)
         on_device = 0
@@ -80,15 +82,15 @@ class DeviceScene:
             import torch
             if accum.dtype != torch.float64 or accum.numel() != nx * ny * 3 or not accum.is_contiguous():
                 raise ValueError("accum must be a contiguous float64 tensor of nx*ny*3")
-            if not accum.is_cuda:
-                raise ValueError("a torch accum must live on the GPU")
+            if not accum.is_cuda or accum.device.index != self.device:
+                raise ValueError(f"a torch accum must live on this scene's GPU (cuda:{self.device})")
             torch.cuda.synchronize(accum.device)
             ptr = C.c_void_p(accum.data_ptr())
             on_device = 1
         prm = _abi.rtw_render_params(nx=nx, ny=ny, spp=spp, max_depth=max_depth, seed=seed, spp_begin=spp_begin,
                                      spp_count=spp_count, row_begin=row_begin, row_step=row_step,
                                      accum_on_device=on_device, collect_kernel_times=int(collect_kernel_times),
-                                     wavefront_paths=wavefront_paths, reserved=0)
+                                     wavefront_paths=wavefront_paths, precision=_precision(precision))
         st = _abi.rtw_stats()
         cam = camera if camera is not None else self.scene.camera
         check(lib().rtw_render_accumulate(self.handle, C.byref(cam), C.byref(prm), ptr, C.byref(st)),
@@ -144,7 +146,8 @@ class DeviceScene:
 
 def render_multi(scenes, nx: int, ny: int, spp: int, max_depth: int, seed: int = 0, *, spp_begin: int = 0,
                  spp_count: int = 0, row_begin: int = 0, row_step: int = 1, accum=None,
-                 camera: Optional[_abi.rtw_camera_desc] = None, collect_kernel_times: bool = False):
+                 camera: Optional[_abi.rtw_camera_desc] = None, collect_kernel_times: bool = False,
+                 precision: str = "fp64"):
     """rtw_render_multi over DeviceScenes on distinct GPUs (one process, one
     host thread per GPU, RCCL reduce to scenes[0]'s device).  `accum`: float64
     numpy array, or torch float64 tensor on scenes[0]'s device."""
@@ -159,6 +162,8 @@ def render_multi(scenes, nx: int, ny: int, spp: int, max_depth: int, seed: int =
         import torch
         if accum.dtype != torch.float64 or accum.numel() != nx * ny * 3 or not accum.is_contiguous():
             raise ValueError("accum must be a contiguous float64 tensor of nx*ny*3")
+        if not accum.is_cuda or accum.device.index != scenes[0].device:
+            raise ValueError(f"a torch accum must live on scenes[0]'s GPU (cuda:{scenes[0].device})")
         torch.cuda.synchronize(accum.device)
         ptr = C.c_void_p(accum.data_ptr())
         on_device = 1
@@ -166,12 +171,19 @@ def render_multi(scenes, nx: int, ny: int, spp: int, max_depth: int, seed: int =
     prm = _abi.rtw_render_params(nx=nx, ny=ny, spp=spp, max_depth=max_depth, seed=seed, spp_begin=spp_begin,
                                  spp_count=spp_count, row_begin=row_begin, row_step=row_step,
                                  accum_on_device=on_device, collect_kernel_times=int(collect_kernel_times),
-                                 wavefront_paths=0, reserved=0)
+                                 wavefront_paths=0, precision=_precision(precision))
     st = _abi.rtw_stats()
     cam = camera if camera is not None else scenes[0].scene.camera
     check(lib().rtw_render_multi(len(scenes), handles, C.byref(cam), C.byref(prm), ptr, C.byref(st)),
           "rtw_render_multi")
     return accum, st.as_dict()
+
+
+def _precision(name: str) -> int:
+    try:
+        return _abi.PRECISIONS[name]
+    except KeyError:
+        raise ValueError(f"precision must be one of {sorted(_abi.PRECISIONS)}, not {name!r}") from None
 
 
 def write_ppm_quantized(path: str, rgb: np.ndarray, nx: int, ny: int) -> None:

@@ -11,9 +11,12 @@ P2="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_V
 P3="SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS"
 P4="FETCH_SIZE GRBM_GUI_ACTIVE"
 P5="WRITE_SIZE GRBM_COUNT"
+# lane utilisation (VALUUtilization = THREAD_CYCLES_VALU / (64 ACTIVE_INST_VALU))
+# and the fp32 / conversion classes of the instruction mix
+P6="SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_CVT GRBM_GUI_ACTIVE"
 i=1
 dirs=()
-for grp in "$P1" "$P2" "$P3" "$P4" "$P5"; do
+for grp in "$P1" "$P2" "$P3" "$P4" "$P5" "$P6"; do
     scripts/prof_pmc.sh "${tag}_$i" "$grp" "$@"
     dirs+=("gpurun_out/pmc_${tag}_$i")
     i=$((i+1))

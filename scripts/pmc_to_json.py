@@ -80,10 +80,25 @@ res = {
         "wait_inst_any (issue stall)": per.get("SQ_WAIT_INST_ANY", 0) / max(1, per.get("SQ_WAVE_CYCLES", 1)),
         "wait_any (waitcnt)": per.get("SQ_WAIT_ANY", 0) / max(1, per.get("SQ_WAVE_CYCLES", 1)),
     },
+    # measured VALU issue: SQ_ACTIVE_INST_VALU is in quad-cycles summed over
+    # the SIMDs, GRBM_GUI_ACTIVE in cycles summed over the 8 XCDs
+    "valu_busy_cycles_per_segment": 4 * per.get("SQ_ACTIVE_INST_VALU", 0) / seg_per_launch if seg_per_launch else None,
+    "valu_busy": (4 * per.get("SQ_ACTIVE_INST_VALU", 0) / 1024) / (per["GRBM_GUI_ACTIVE"] / 8)
+    if per.get("GRBM_GUI_ACTIVE") else None,
+    "clock_ghz_x_ms": per.get("GRBM_GUI_ACTIVE", 0) / 8 / 1e6,
+    # lanes doing work per VALU instruction cycle (rocprof's VALUUtilization):
+    # the divergence measure the VALU fraction alone cannot show
+    "valu_lane_util": per["SQ_THREAD_CYCLES_VALU"] / (64 * per["SQ_ACTIVE_INST_VALU"])
+    if per.get("SQ_THREAD_CYCLES_VALU") and per.get("SQ_ACTIVE_INST_VALU") else None,
+    "f32_insts_per_wave_segment": {k[14:]: per.get(k, 0) / wave_segments for k in
+                                   ("SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32",
+                                    "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_CVT", "SQ_INSTS_VALU_INT32",
+                                    "SQ_INSTS_VALU_INT64")} if wave_segments else None,
     "waves_per_launch": per.get("SQ_WAVES"),
     "raw_per_launch": per,
 }
 Path(out).parent.mkdir(parents=True, exist_ok=True)
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: res[k] for k in ("kernel", "build_id", "workload", "hbm_bytes_per_launch",
-                                      "valu_insts_per_wave_segment", "wave_cycle_split")}))
+                                      "valu_insts_per_wave_segment", "valu_busy", "valu_lane_util",
+                                      "wave_cycle_split")}))

@@ -6,6 +6,7 @@
 #include <cfloat>
 #include <cstdio>
 #include <memory>
+#include <string>
 #include "rtw/scene.h"
 
 static int failures = 0;
@@ -100,6 +101,21 @@ int main() {
     if (d2) {
         CHECK(d2->n_entries == 1 && d2->entries[0].n_prims == 20 && d2->entries[0].bvh_root >= 0);
         rtw_scene_desc_free(d2);
+    }
+    // a bvh_node holding a constant_medium: the reference's bvh_node::hit is
+    // broken (hittable.h:82-110), no walk order to reproduce -> refused
+    {
+        std::vector<std::shared_ptr<hittable>> kids;
+        kids.push_back(std::make_shared<sphere>(vec3(0, 0, 0), 1.0, mat));
+        kids.push_back(std::make_shared<constant_medium>(
+            std::make_shared<sphere>(vec3(3, 0, 0), 1.0, mat), 0.1,
+            std::make_shared<isotropic>(std::make_shared<constant_texture>(vec3(1, 1, 1)))));
+        scene sm;
+        sm.Add(std::make_shared<bvh_node>(kids, 0.0, 1.0));
+        rtw_scene_desc* d3 = nullptr;
+        CHECK(rtw_flatten_scene(sm, 0, &d3) == RTW_ERR_UNSUPPORTED);
+        CHECK(d3 == nullptr);
+        CHECK(std::string(rtw_last_error()).find("bvh_node") != std::string::npos);
     }
     std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
     return failures ? 1 : 0;

@@ -95,6 +95,77 @@ def test_error_reporting_without_device(built):
     assert lib.rtw_render_accumulate(None, None, None, None, None) == -1
 
 
+def _bad_owner_desc(sd, mutate):
+    """A copy of sd's desc whose prim array is a private copy changed by
+    `mutate(prims)` (the library-owned arrays stay untouched)."""
+    d = _abi.rtw_scene_desc.from_buffer_copy(sd.desc)
+    prims = (_abi.rtw_prim * d.n_prims)()
+    C.memmove(prims, d.prims, C.sizeof(prims))
+    mutate(prims)
+    d.prims = C.cast(prims, C.POINTER(_abi.rtw_prim))
+    return d, prims
+
+
+def test_upload_rejects_prims_their_entries_do_not_own(built):
+    """validate_desc's ownership rule (rtw_kernels.hip validate_desc): every
+    prim of an entry's range names that entry, and a light's own copy names
+    none -- hit_record reads the winner's transforms through prims[i].entry,
+    so a desc breaking it would index entries out of their range."""
+    lib = _abi.lib()
+    from raytracingweekend_amd.render import SceneDesc
+    sd = SceneDesc("cornell_box", 1.0)
+    h = C.c_void_p()
+    e0 = sd.desc.entries[0]
+    # a prim inside entry 0's range naming entry 1
+    d, keep = _bad_owner_desc(sd, lambda P: setattr(P[e0.first_prim], "entry", 1))
+    assert lib.rtw_scene_upload(0, C.byref(d), C.byref(h)) == -1
+    assert b"lies in entry" in lib.rtw_last_error() and h.value is None
+    # a light's own copy (outside every range) claiming an entry
+    n = sd.desc.n_prims
+    d, keep = _bad_owner_desc(sd, lambda P: setattr(P[n - 1], "entry", 0))
+    assert lib.rtw_scene_upload(0, C.byref(d), C.byref(h)) == -1
+    assert b"names entry" in lib.rtw_last_error()
+    # an entry index past the end
+    d, keep = _bad_owner_desc(sd, lambda P: setattr(P[0], "entry", sd.desc.n_entries))
+    assert lib.rtw_scene_upload(0, C.byref(d), C.byref(h)) == -1
+    assert b"entry out of range" in lib.rtw_last_error()
+    # two entries claiming one prim
+    bad = _abi.rtw_scene_desc.from_buffer_copy(sd.desc)
+    ents = (_abi.rtw_entry * bad.n_entries)()
+    C.memmove(ents, bad.entries, C.sizeof(ents))
+    ents[1].first_prim = ents[0].first_prim
+    ents[1].n_prims = 1
+    bad.entries = C.cast(ents, C.POINTER(_abi.rtw_entry))
+    assert lib.rtw_scene_upload(0, C.byref(bad), C.byref(h)) == -1
+    assert b"belongs to entries" in lib.rtw_last_error()
+
+
+def test_render_multi_argument_errors(built):
+    """rtw_render_multi refuses bad arguments before touching any device."""
+    lib = _abi.lib()
+    from raytracingweekend_amd.render import SceneDesc
+    sd = SceneDesc("cornell_box", 1.0)
+    prm = _abi.rtw_render_params(nx=8, ny=8, spp=1, max_depth=5, row_step=1)
+    acc = np.zeros(8 * 8 * 3)
+    hs = (C.c_void_p * 2)(None, None)
+    for n in (0, -1):
+        assert lib.rtw_render_multi(n, hs, C.byref(sd.camera), C.byref(prm), acc.ctypes.data_as(C.c_void_p),
+                                    None) == -1
+    assert lib.rtw_render_multi(2, hs, C.byref(sd.camera), C.byref(prm), acc.ctypes.data_as(C.c_void_p),
+                                None) == -1
+    assert b"null scene handle" in lib.rtw_last_error()
+    assert lib.rtw_render_multi(1, None, C.byref(sd.camera), C.byref(prm), acc.ctypes.data_as(C.c_void_p),
+                                None) == -1
+
+
+def test_precision_names():
+    from raytracingweekend_amd.render import _precision
+    assert _precision("fp64") == _abi.RTW_PRECISION_FP64 == 0
+    assert _precision("fp32") == _abi.RTW_PRECISION_FP32 == 1
+    with pytest.raises(ValueError):
+        _precision("bf16")
+
+
 def test_library_refuses_to_fall_back(tmp_path):
     """A missing librtw.so is an error, never a silent CPU path."""
     import os

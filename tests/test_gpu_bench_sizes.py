@@ -174,3 +174,94 @@ def test_scene_query_names_the_launched_kernel(gpu):
     assert info["kernel"].startswith("k_persist_sort<")
     assert info["build_id"] == gpu.build_id() and info["build_id"] != "unknown"
     assert info["n_world_runs"] >= 1 and info["shade_lds_bytes"] > 0
+
+
+def test_multi_pass_at_C5_resolution(gpu, monkeypatch):
+    """The whole C5 image (Book-2 final, 1600x1600, BVH) at 16 of its 4096
+    samples, forced through 4 passes of 4 samples per pixel (the full config
+    runs 10 passes of 2^30 samples): every pixel rendered (sample counts,
+    finite radiance), traversals per sample where the one-pass render and the
+    bench put them (~5.62), and the multi-pass accumulator bit-identical to the
+    one-pass one (per-pixel running sums carried across passes in sample
+    order, RayTracingWeekend.cpp:235-239)."""
+    nx, ny, spp, depth, cnt = 1600, 1600, 4096, 50, 16
+    sd = gpu.SceneDesc("book2_final", 1.0, use_bvh=True)
+    ds = gpu.DeviceScene(sd)
+    try:
+        one, st1 = ds.render_accumulate(nx, ny, spp, depth, 0, spp_begin=spp - cnt, spp_count=cnt)
+        monkeypatch.setenv("RTW_PASS_SAMPLES", str(nx * ny * 4))
+        many, st4 = ds.render_accumulate(nx, ny, spp, depth, 0, spp_begin=spp - cnt, spp_count=cnt)
+    finally:
+        ds.close()
+    assert st1["launches_intersect"] == 1 and st4["launches_intersect"] == 4
+    assert st1["samples"] == st4["samples"] == nx * ny * cnt
+    assert st1["segments"] == st4["segments"]
+    assert 5.4 < st4["segments"] / st4["samples"] < 5.85
+    assert np.all(np.isfinite(many))
+    assert np.array_equal(one, many)
+    lum = many.reshape(-1, 3).sum(axis=1)
+    assert (lum > 0).mean() > 0.5  # a lit image, not a zeroed buffer
+
+
+def test_render_multi_rejects_bad_handles_and_accumulators(gpu):
+    """rtw_render_multi: two handles on one device are refused, and so is a
+    device accumulator that is not device memory of handles[0]'s GPU
+    (rtw_render_accumulate likewise)."""
+    import ctypes as C
+    import torch
+    from raytracingweekend_amd import _abi
+    nx, ny, spp = 16, 16, 2
+    sd = gpu.SceneDesc("cornell_box", 1.0)
+    a, b = gpu.DeviceScene(sd), gpu.DeviceScene(sd)
+    L = gpu.lib()
+    try:
+        with pytest.raises(_abi.RtwError, match="two handles on one device"):
+            gpu.render_multi([a, b], nx, ny, spp, 10)
+        hs = (C.c_void_p * 1)(a.handle.value)
+        prm = _abi.rtw_render_params(nx=nx, ny=ny, spp=spp, max_depth=10, row_step=1, accum_on_device=1)
+        host = np.zeros(nx * ny * 3)
+        assert L.rtw_render_multi(1, hs, C.byref(sd.camera), C.byref(prm), host.ctypes.data_as(C.c_void_p),
+                                  None) == -1
+        assert b"not device memory" in L.rtw_last_error()
+        assert L.rtw_render_accumulate(a.handle, C.byref(sd.camera), C.byref(prm), host.ctypes.data_as(C.c_void_p),
+                                       None) == -1
+        assert b"not device memory" in L.rtw_last_error()
+        prm.accum_on_device, prm.precision = 0, 7
+        assert L.rtw_render_accumulate(a.handle, C.byref(sd.camera), C.byref(prm), host.ctypes.data_as(C.c_void_p),
+                                       None) == -1
+        assert b"precision" in L.rtw_last_error()
+        with pytest.raises(ValueError):
+            a.render_accumulate(nx, ny, spp, 10, accum=torch.zeros(nx * ny * 3, dtype=torch.float64))
+    finally:
+        L.rtw_release_communicators()
+        a.close()
+        b.close()
+
+
+@pytest.mark.skipif("not __import__('torch').cuda.is_available() or __import__('torch').cuda.device_count() < 2",
+                    reason="needs two or more GPUs")
+def test_render_multi_across_gpus_matches_one_gpu(gpu):
+    """rtw_render_multi over every visible GPU (one host thread per device,
+    ncclCommInitAll, grouped ncclReduce): equal to rtw_render_accumulate of the
+    whole sample range within fp64 reassociation of the shard sums, host and
+    device accumulators, with the same sample and traversal counts."""
+    import torch
+    n = min(torch.cuda.device_count(), 8)
+    nx, ny, spp, depth = 96, 64, 2 * n + 1, 50
+    sd = gpu.SceneDesc("cornell_box", nx / ny)
+    scenes = [gpu.DeviceScene(sd, g) for g in range(n)]
+    try:
+        ref, st_ref = scenes[0].render_accumulate(nx, ny, spp, depth, 3)
+        got, st = gpu.render_multi(scenes, nx, ny, spp, depth, 3)
+        assert st["samples"] == st_ref["samples"] and st["segments"] == st_ref["segments"]
+        assert np.allclose(got, ref, rtol=1e-13, atol=1e-13)
+        dev = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda:0")
+        gpu.render_multi(scenes, nx, ny, spp, depth, 3, accum=dev)
+        assert np.allclose(dev.cpu().numpy(), ref, rtol=1e-13, atol=1e-13)
+        with pytest.raises(ValueError):
+            gpu.render_multi(scenes, nx, ny, spp, depth, 3,
+                             accum=torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda:1"))
+    finally:
+        gpu.lib().rtw_release_communicators()
+        for s in scenes:
+            s.close()
