@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--bvh", action="store_true", default=None)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32"],
+                    help="fp64: the reference's double arithmetic (parity mode, the headline); fp32: the fast "
+                         "mode, statistical parity only, reported as its own line")
     ap.add_argument("--paths", type=int, default=0, help="wavefront paths in flight (0 = library default)")
     ap.add_argument("--no-kernel-times", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -106,9 +109,10 @@ def parse():
 
 def pmc_key(args) -> str:
     """What a PMC record must have been taken on: per-segment instruction
-    counts and per-launch bytes depend on the scene, image and depth (spp and
-    GPU count only scale them)."""
-    return f"{args.scene} {args.nx}x{args.ny} depth {args.depth}" + (" bvh" if args.bvh else "")
+    counts and per-launch bytes depend on the scene, image, depth and
+    precision (spp and GPU count only scale them)."""
+    return (f"{args.scene} {args.nx}x{args.ny} depth {args.depth}" + (" bvh" if args.bvh else "") +
+            (" fp32" if getattr(args, "precision", "fp64") == "fp32" else ""))
 
 
 def find_pmc(kernel: str, build: str, key: str, pmc_dir: Path = PMC_DIR):
@@ -188,8 +192,8 @@ def roofline(args, kernel, build, seg, ms, launches, algo):
     hbm = {"achieved": round(hbm_ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(hbm_ach / HBM_PEAK_GBS, 4), "bytes_per_segment": round(algo / max(seg, 1), 2),
            "algo_bytes_per_launch": round(algo / max(launches, 1), 1),
-           "definition": "SURVEY.md 8(d): 68 algorithmic bytes per traversal (ray 56 B in, hit 12 B out) x "
-                         "device-counted traversals / HIP-event launch time"}
+           "definition": "SURVEY.md 8(d): 68 algorithmic bytes per traversal in fp64 (ray 56 B in, hit 12 B out; "
+                         "36 B in the fp32 fast mode) x device-counted traversals / HIP-event launch time"}
     rec, src = find_pmc(kernel, build, pmc_key(args))
     out = {"kernel": kernel, "build_id": build, "launches": int(launches), "avg_launch_ms": round(avg_ms, 4),
            "segments_per_launch": round(seg_launch, 1)}
@@ -263,7 +267,7 @@ def main():
 
     def step(timed: bool):
         fn = gpu_render_fn(ds, nx, ny, spp_total, depth, args.seed, collect_kernel_times=collect and timed,
-                           wavefront_paths=args.paths)
+                           wavefront_paths=args.paths, precision=args.precision)
         return render_step(fn, gpu_finalize_fn(ds, nx, ny, spp_total), accum, canvas, nx, ny, spp_total)
 
     for _ in range(args.warmup):
@@ -298,18 +302,20 @@ def main():
         samples_per_step = nx * ny * spp_total
         assert int(samples) == samples_per_step * args.steps, "ranks rendered a different number of samples"
         value = samples_per_step * args.steps / elapsed / 1e6
-        roof = roofline(args, info["kernel"], info["build_id"], seg, ms_isect, launches, algo) \
+        kernel = info["kernel_fast"] if args.precision == "fp32" else info["kernel"]
+        roof = roofline(args, kernel, info["build_id"], seg, ms_isect, launches, algo) \
             if collect and ms_isect > 0 else None
         if roof:
             roof["bvh_lds_nodes"] = info["bvh_lds_nodes"]  # BVH node packet staged in LDS per workgroup
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
+            "dtype": "f32" if args.precision == "fp32" else "f64",
             "data": "synthetic (the reference's own scene definitions, seeded RNG)",
             "config": {"workload": args.label, "workload_id": args.workload_key, "scene": args.scene, "nx": nx,
                        "ny": ny, "spp_total": spp_total, "spp_per_gpu": spp_total / world, "max_depth": depth,
-                       "bvh": args.bvh, "global_batch": samples_per_step,
+                       "bvh": args.bvh, "precision": args.precision, "global_batch": samples_per_step,
                        "parallelism": f"spp-shard x{world}" + (" + RCCL reduce" if world > 1 else "")},
             "msegments_per_s": round(seg / elapsed / 1e6, 2) if seg else None,
             "segments_per_sample": round(seg / max(samples, 1), 4),

@@ -113,7 +113,13 @@ typedef struct rtw_entry {
 } rtw_entry; /* 312 bytes */
 
 /* BVH node: internal when count == 0 (children left/right), leaf when
- * count > 0 (items bvh_items[left .. left+count)). */
+ * count > 0 (items bvh_items[left .. left+count)).  Items of a group BVH are
+ * prim indices of the group, or RTW_ITEM_BOX | i for the six rects
+ * [i, i+6) of one box (hittable_list.h:65-114: xy, xy, xz, xz, yz, yz in that
+ * list order), tested together as one leaf object; items of the world BVH
+ * are entry indices. */
+#define RTW_ITEM_BOX 0x40000000
+#define RTW_ITEM_INDEX 0x3fffffff
 typedef struct rtw_bvh_node {
     double bmin[3];
     double bmax[3];
@@ -336,6 +342,8 @@ typedef struct rtw_scene_info {
                                  launches now, e.g. "k_persist_sort<112, 8, true>"
                                  (RTW_MODE / RTW_SORT / RTW_SPLIT respected) */
     char build_id[48];        /* hash of the device code's sources and flags  */
+    char kernel_fast[128];    /* traversal kernel of a precision = FP32 render,
+                                 e.g. "k_fast<0, false>"                     */
 } rtw_scene_info;
 
 int rtw_scene_query(void* scene_handle, rtw_scene_info* out);

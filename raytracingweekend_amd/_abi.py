@@ -26,6 +26,8 @@ RTW_LIGHT_DEFAULT, RTW_LIGHT_XZ_RECT, RTW_LIGHT_SPHERE = range(3)
 RTW_RENDER_SHADED, RTW_RENDER_NORMAL = 0, 1
 RTW_BG_BLACK, RTW_BG_GRADIENT = 0, 1
 RTW_PRECISION_FP64, RTW_PRECISION_FP32 = 0, 1
+RTW_ITEM_BOX, RTW_ITEM_INDEX = 0x40000000, 0x3FFFFFFF
+RTW_VISIT_REPLAY, RTW_VISIT_ENTRY = 0x40000000, 0x3FFFFFFF
 PRECISIONS = {"fp64": RTW_PRECISION_FP64, "fp32": RTW_PRECISION_FP32}
 
 
@@ -99,12 +101,12 @@ class rtw_scene_info(C.Structure):
     _fields_ = [("device", C.c_int32), ("n_world_runs", C.c_int32), ("n_ysphere_runs", C.c_int32),
                 ("n_plain_runs", C.c_int32), ("features", C.c_int32), ("shade_mask", C.c_int32),
                 ("shade_lds_bytes", C.c_int32), ("bvh_lds_nodes", C.c_int32), ("kernel", C.c_char * 128),
-                ("build_id", C.c_char * 48)]
+                ("build_id", C.c_char * 48), ("kernel_fast", C.c_char * 128)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
-        d["kernel"] = d["kernel"].decode()
-        d["build_id"] = d["build_id"].decode()
+        for k in ("kernel", "build_id", "kernel_fast"):
+            d[k] = d[k].decode()
         return d
 
 

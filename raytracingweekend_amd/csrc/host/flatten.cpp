@@ -31,6 +31,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 #include "rtw/flatten.h"
@@ -170,6 +171,7 @@ struct flattener {
     std::vector<int32_t> items;
     std::map<const material*, int> mat_ids;
     std::map<const texture*, int> tex_ids;
+    std::set<int> box_starts;  // first prims of boxes' six-rect runs
     bool perlin = false;
     std::string err;
     bool nesting = false;  // collect() met a transform or medium
@@ -294,7 +296,18 @@ struct flattener {
             return true;
         }
         if (auto f = dynamic_cast<const flip_normals*>(h)) return collect(f->ptr.get(), flip + 1, entry);
-        if (auto b = dynamic_cast<const box*>(h)) return collect(&b->list_ptr, flip, entry);
+        if (auto b = dynamic_cast<const box*>(h)) {
+            const size_t first = prims.size();
+            if (!collect(&b->list_ptr, flip, entry)) return false;
+            // a box's six rects in its list order (hittable_list.h:65-114):
+            // one item of a group BVH (RTW_ITEM_BOX)
+            static const int kBoxTypes[6] = {RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XZ,
+                                             RTW_PRIM_RECT_XZ, RTW_PRIM_RECT_YZ, RTW_PRIM_RECT_YZ};
+            bool is_box = prims.size() == first + 6;
+            for (int j = 0; j < 6 && is_box; ++j) is_box = prims[first + j].type == kBoxTypes[j];
+            if (is_box) box_starts.insert((int)first);
+            return true;
+        }
         if (auto l = dynamic_cast<const hittable_list*>(h)) {
             for (const auto& o : l->objects)
                 if (!collect(o.get(), flip, entry)) return false;
@@ -603,6 +616,11 @@ int rtw_flatten_world(const hittable_list& world, const hittable_list* lights, c
         };
         const int leaf_max = env_leaf("RTW_BVH_LEAF_MAX", 2);
         const int world_leaf_max = env_leaf("RTW_BVH_WORLD_LEAF_MAX", 1);
+        // a box is one BVH item (its six rects tested together in list
+        // order) rather than six: a third of the nodes for a group of boxes
+        // (RTW_BVH_BOX_ITEMS=0: six items, for A/B)
+        const char* bx = std::getenv("RTW_BVH_BOX_ITEMS");
+        const bool box_items = !(bx && *bx && std::atoi(bx) == 0);
         // group BVHs over large groups
         for (auto& e : f.entries) {
             if (e.n_prims <= 8) continue;
@@ -611,6 +629,15 @@ int rtw_flatten_world(const hittable_list& world, const hittable_list* lights, c
                 bvh_item it;
                 f.prim_bounds(f.prims[i], it.lo, it.hi);
                 it.id = i;
+                if (box_items && f.box_starts.count(i) && i + 6 <= e.first_prim + e.n_prims) {
+                    for (int j = 1; j < 6; ++j) {
+                        double lo[3], hi[3];
+                        f.prim_bounds(f.prims[i + j], lo, hi);
+                        for (int k = 0; k < 3; ++k) it.lo[k] = std::min(it.lo[k], lo[k]), it.hi[k] = std::max(it.hi[k], hi[k]);
+                    }
+                    it.id = i | RTW_ITEM_BOX;
+                    i += 5;
+                }
                 its.push_back(it);
             }
             bvh_builder b{f.nodes, f.items, leaf_max};

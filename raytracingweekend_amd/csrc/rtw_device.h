@@ -806,6 +806,37 @@ RTW_D void arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_sta
     }
 }
 
+// A box item of a group BVH (RTW_ITEM_BOX): its six rects in the box's list
+// order (hittable_list.h:65-114: +z, -z, +y, -y, +x, -x), each with the
+// reference's own test and better()'s tie rule -- exactly six arbitrate
+// calls, with each rect's plane axis known instead of read from its type.
+template <int K, int A, int B>
+RTW_D void rect_arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_state& h) {
+    const rtw_prim& q = S.prims[pi];  // fields read where the test uses them
+    double t;
+    if (!rect_axis_t<K, A, B>(q, r, t_min, h.t, t)) return;
+    if (better(t, pi, true, h.t, h.prim, h.rect, h.prim != -1)) {
+        h.t = t;
+        h.prim = pi;
+        h.rect = true;
+    }
+}
+RTW_D void box_arbitrate(const scene& S, int first, const ray& r, double t_min, hit_state& h) {
+    rect_arbitrate<2, 0, 1>(S, first, r, t_min, h);
+    rect_arbitrate<2, 0, 1>(S, first + 1, r, t_min, h);
+    rect_arbitrate<1, 0, 2>(S, first + 2, r, t_min, h);
+    rect_arbitrate<1, 0, 2>(S, first + 3, r, t_min, h);
+    rect_arbitrate<0, 1, 2>(S, first + 4, r, t_min, h);
+    rect_arbitrate<0, 1, 2>(S, first + 5, r, t_min, h);
+}
+// a group-BVH leaf item: a prim, or a box's six rects
+RTW_D void arbitrate_item(const scene& S, int it, const ray& r, double t_min, hit_state& h, double fc) {
+    if (it & RTW_ITEM_BOX)
+        box_arbitrate(S, it & RTW_ITEM_INDEX, r, t_min, h);
+    else
+        arbitrate(S, it, r, t_min, h, fc);
+}
+
 // arbitrate for a world walk's one-prim leaves with the walk's shared
 // 1 / dot(d, d) (walk_quot's rules; t_min = 0.001)
 RTW_D void arbitrate_a(const scene& S, int pi, const ray& r, double t_min, hit_state& h, double fc, double ya,
@@ -1012,7 +1043,7 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
             if (lc == 0 && sp + 2 <= STK::cap) push_children(nd, dneg, stk, sp);
         }
         if (lc == 0) break;
-        for (int k = 0; k < lc; ++k) arbitrate(S, S.items[la + k], r, t_min, h, fc);
+        for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
     }
 #else
     stk.at(sp++) = root;
@@ -1021,7 +1052,7 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
         if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
         const int cnt = node_count(nd);
         if (cnt > 0) {
-            for (int k = 0; k < cnt; ++k) arbitrate(S, S.items[nd.a + k], r, t_min, h, fc);
+            for (int k = 0; k < cnt; ++k) arbitrate_item(S, S.items[nd.a + k], r, t_min, h, fc);
         } else if (sp + 2 <= STK::cap) {  // always true: depth checked at upload
             push_children(nd, dneg, stk, sp);
         }

@@ -33,6 +33,7 @@
 #include <tuple>
 #include <vector>
 #include "rtw_device.h"
+#include "rtw_fast.h"
 #include "host/rtw_host_util.h"
 
 using namespace rtwd;
@@ -100,13 +101,31 @@ struct job_t {
     uint32_t total;      // samples in this pass
     uint32_t npix;       // pixels of this call (n_rows * nx)
     int32_t nx, ny, row_begin, row_step, s_begin, max_depth;
+    uint32_t spp_pass;   // samples per pixel in this pass
     double* L;           // per-sample radiance, L[3q + c] (pass-local sample id q)
 };
 
+// Pass-local sample ids are pixel-major (RTW_PIXEL_MAJOR): q = pixel *
+// spp_pass + sample, so the 64 ids a wave reserves are 64 samples of one
+// pixel and their 24-byte radiance records fill whole cache lines of one
+// contiguous 1.5 KB run (sample-major ids scattered them over 64 pixels'
+// planes: partial-sector writes, 1.55x the record bytes); k_reduce then
+// reads each pixel's records as one contiguous run.  Results do not depend
+// on it: the RNG is keyed by (pixel, sample) and each pixel's records are
+// still summed in increasing sample order.
+#ifndef RTW_PIXEL_MAJOR
+#define RTW_PIXEL_MAJOR 1
+#endif
+
 // pass-local sample id -> pixel (i, j) and global sample index s
 __device__ __forceinline__ void sample_coords(const job_t& J, uint32_t q, int& i, int& j, int& s) {
+#if RTW_PIXEL_MAJOR
+    const uint32_t rem = q / J.spp_pass;
+    const uint32_t sl = q - rem * J.spp_pass;
+#else
     const uint32_t sl = q / J.npix;
     const uint32_t rem = q - sl * J.npix;
+#endif
     const uint32_t k = rem / (uint32_t)J.nx;
     i = (int)(rem - k * (uint32_t)J.nx);
     j = J.row_begin + (int)k * J.row_step;
@@ -659,12 +678,29 @@ __device__ __forceinline__ const persist_args& args_now() {
 }
 
 // LST: BVH traversal stacks in LDS (one column per lane) instead of scratch.
+//
+// DIRECT (RTW_PERSIST_DIRECT): the heavy kernels (media scenes: ~10 000 VALU
+// instructions per wave-segment, where a camera ray is ~1 %) take camera
+// samples straight into the idle lanes -- no per-wave batch -- and spend the
+// batch's 16 KB of LDS on a slot per lane holding the path's ray between
+// iterations: read before traversal, read again before shading (so it is not
+// live in registers across the walk), and the continuation written there.
+// In registers that loop-carried ray was what the Book-2 kernel spilled to
+// scratch (9 VGPRs, 48 bytes per lane, most of its HBM write traffic).
+// Measured (1 MI355X, A/B): C5 slice 577 vs 617 Msamples/s, C3 2617 vs
+// 2711 -- the lane-partial camera sampling costs more than the spills it
+// removes, so it is off (-DRTW_PERSIST_DIRECT(F)=1 selects it).
+#ifndef RTW_PERSIST_DIRECT
+#define RTW_PERSIST_DIRECT(F) 0
+#endif
 template <int F, int M, bool LDS, bool LST = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist(persist_args) {
+    constexpr bool DIRECT = RTW_PERSIST_DIRECT(F);
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kWaves];
-    __shared__ ray_batch s_batch[kWaves];
+    __shared__ ray_batch s_batch[DIRECT ? 1 : kWaves];
+    __shared__ double s_ray[DIRECT ? 7 : 1][kBlock];  // DIRECT: each lane's ray (o, d, time)
     __shared__ double s_thr[3][kBlock];  // each lane's path throughput
     __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kBlock];
     __shared__ uint32_t s_q[kBlock];     // each lane's sample id
@@ -690,6 +726,16 @@ void k_persist(persist_args) {
     uint32_t bl = 0, bh = 0;  // wave-uniform: unread batch entries [bl, bh)
     uint32_t segs = 0;
     prof_t pf;
+    // the lane's parked ray (DIRECT)
+    auto park = [&](uint32_t me, const ray& r) {
+        s_ray[0][me] = r.o.x, s_ray[1][me] = r.o.y, s_ray[2][me] = r.o.z;
+        s_ray[3][me] = r.d.x, s_ray[4][me] = r.d.y, s_ray[5][me] = r.d.z;
+        if (!(F & F_STATIC)) s_ray[6][me] = r.t;
+    };
+    auto unpark = [&](uint32_t me) {
+        return ray{d3{s_ray[0][me], s_ray[1][me], s_ray[2][me]}, d3{s_ray[3][me], s_ray[4][me], s_ray[5][me]},
+                   (F & F_STATIC) ? 0.0 : s_ray[6][me]};
+    };
     for (;;) {
         // lane-dependent LDS addresses (batch, throughput, sample id, stack
         // columns) are formed from an opaque copy of the thread index where
@@ -698,19 +744,16 @@ void k_persist(persist_args) {
         uint32_t tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         const uint32_t ln = tid & 63;
-        // (the wave's batch too: formed once per kernel, its per-array
-        // addresses were held in 15 VGPRs across the whole loop)
-        ray_batch& B = s_batch[tid >> 6];
-        for (int round = 0; round < 2; ++round) {
-            const unsigned long long m = __ballot(x.depth == 0);
-            if (!m) break;
-            if (bl == bh) {
-                if (!open) break;
+        if constexpr (DIRECT) {
+            // idle lanes take new camera samples, one reservation per wave
+            const bool idle = x.depth == 0;
+            const unsigned long long m = __ballot(idle);
+            if (open && m) {
                 const persist_args& A = args_now();
                 const job_t& J = A.J;
                 ctrs_t* const C = A.C;
-                // reserve up to 64 ids, own shard first
-                uint32_t left = 64, given = 0, q = 0;
+                const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+                uint32_t left = (uint32_t)__popcll(m), given = 0, q = 0;
                 bool got = false;
                 for (int a = 0; a < kQShards && left; ++a) {
                     const int sh = (own + a) % kQShards;
@@ -724,8 +767,8 @@ void k_persist(persist_args) {
                     b = __shfl(b, 0, 64);
                     if (b == ~0ull || b >= lim) continue;
                     const uint32_t ok = (uint32_t)min((unsigned long long)left, lim - b);
-                    if (ln >= given && ln < given + ok) {
-                        q = (uint32_t)shard_sample(sh, b + (ln - given));
+                    if (idle && rank >= given && rank < given + ok) {
+                        q = (uint32_t)shard_sample(sh, b + (rank - given));
                         got = true;
                     }
                     given += ok;
@@ -733,35 +776,79 @@ void k_persist(persist_args) {
                 }
                 if (left) open = false;
                 if (got) {
-                    uint32_t rng;
-                    const ray r = camera_sample(J, q, rng);
-                    B.ox[ln] = r.o.x, B.oy[ln] = r.o.y, B.oz[ln] = r.o.z;
-                    B.dx[ln] = r.d.x, B.dy[ln] = r.d.y, B.dz[ln] = r.d.z;
-                    B.tm[ln] = r.t;
-                    B.rng[ln] = rng;
-                    B.q[ln] = q;
+                    park(tid, camera_sample(J, q, x.rng));
+                    s_q[tid] = q;
+                    s_thr[0][tid] = 1.0, s_thr[1][tid] = 1.0, s_thr[2][tid] = 1.0;
+                    x.depth = (uint32_t)J.max_depth;
                 }
-                bl = 0;
-                bh = given;
-                if (!bh) break;
+            }
+        } else {
+            // (the wave's batch too: formed once per kernel, its per-array
+            // addresses were held in 15 VGPRs across the whole loop)
+            ray_batch& B = s_batch[tid >> 6];
+            for (int round = 0; round < 2; ++round) {
+                const unsigned long long m = __ballot(x.depth == 0);
+                if (!m) break;
+                if (bl == bh) {
+                    if (!open) break;
+                    const persist_args& A = args_now();
+                    const job_t& J = A.J;
+                    ctrs_t* const C = A.C;
+                    // reserve up to 64 ids, own shard first
+                    uint32_t left = 64, given = 0, q = 0;
+                    bool got = false;
+                    for (int a = 0; a < kQShards && left; ++a) {
+                        const int sh = (own + a) % kQShards;
+                        const unsigned long long lim = shard_limit(sh, J.total);
+                        unsigned long long b = ~0ull;
+                        if (ln == 0) {
+                            const bool dry = a > 0 && __hip_atomic_load(&C->qshard[sh].v, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT) >= lim;
+                            if (!dry) b = atomicAdd(&C->qshard[sh].v, (unsigned long long)left);
+                        }
+                        b = __shfl(b, 0, 64);
+                        if (b == ~0ull || b >= lim) continue;
+                        const uint32_t ok = (uint32_t)min((unsigned long long)left, lim - b);
+                        if (ln >= given && ln < given + ok) {
+                            q = (uint32_t)shard_sample(sh, b + (ln - given));
+                            got = true;
+                        }
+                        given += ok;
+                        left -= ok;
+                    }
+                    if (left) open = false;
+                    if (got) {
+                        uint32_t rng;
+                        const ray r = camera_sample(J, q, rng);
+                        B.ox[ln] = r.o.x, B.oy[ln] = r.o.y, B.oz[ln] = r.o.z;
+                        B.dx[ln] = r.d.x, B.dy[ln] = r.d.y, B.dz[ln] = r.d.z;
+                        B.tm[ln] = r.t;
+                        B.rng[ln] = rng;
+                        B.q[ln] = q;
+                    }
+                    bl = 0;
+                    bh = given;
+                    if (!bh) break;
+                    __builtin_amdgcn_wave_barrier();
+                }
+                const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+                const uint32_t avail = bh - bl;
+                if (x.depth == 0 && rank < avail) {
+                    const uint32_t k = bl + rank;
+                    x.r = ray{d3{B.ox[k], B.oy[k], B.oz[k]}, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
+                    x.rng = B.rng[k];
+                    s_q[tid] = B.q[k];
+                    s_thr[0][tid] = 1.0, s_thr[1][tid] = 1.0, s_thr[2][tid] = 1.0;
+                    x.depth = (uint32_t)args_now().J.max_depth;
+                }
+                bl += min((uint32_t)__popcll(m), avail);
                 __builtin_amdgcn_wave_barrier();
             }
-            const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
-            const uint32_t avail = bh - bl;
-            if (x.depth == 0 && rank < avail) {
-                const uint32_t k = bl + rank;
-                x.r = ray{d3{B.ox[k], B.oy[k], B.oz[k]}, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
-                x.rng = B.rng[k];
-                s_q[tid] = B.q[k];
-                s_thr[0][tid] = 1.0, s_thr[1][tid] = 1.0, s_thr[2][tid] = 1.0;
-                x.depth = (uint32_t)args_now().J.max_depth;
-            }
-            bl += min((uint32_t)__popcll(m), avail);
-            __builtin_amdgcn_wave_barrier();
         }
         if (!__any(x.depth != 0)) break;
         pf.mark(PS_LOAD);
         if (x.depth != 0) {
+            if constexpr (DIRECT) x.r = unpark(tid);
             const persist_args& A = args_now();
             scene S = A.S;
             hit_state h;
@@ -783,7 +870,13 @@ void k_persist(persist_args) {
                                                         : SS.prims[h.prim].material].type);
 #endif
             // the outcome is applied inside the branch that produced it
-            const uint32_t me = tid;
+            uint32_t me = tid;
+            if constexpr (DIRECT) {
+                // the ray again from its slot: the copy the walk used is dead
+                // from here on (a fresh index keeps the compiler from reusing it)
+                asm volatile("" : "+v"(me)::"memory");
+                x.r = unpark(me);
+            }
             auto radiance = [&](const d3& L) {
                 double* o = A2.J.L + 3 * (size_t)s_q[me];
                 o[0] = L.x, o[1] = L.y, o[2] = L.z;
@@ -792,7 +885,10 @@ void k_persist(persist_args) {
             auto sk = make_sink(
                 [&](const d3& f, const ray& r) {
                     s_thr[0][me] *= f.x, s_thr[1][me] *= f.y, s_thr[2][me] *= f.z;
-                    nr = r;
+                    if constexpr (DIRECT)
+                        park(me, r);  // the continuation waits in the lane's slot
+                    else
+                        nr = r;
                 },
                 [&](const d3& E) { radiance(d3{s_thr[0][me], s_thr[1][me], s_thr[2][me]} * E); },
                 [&]() {
@@ -801,10 +897,10 @@ void k_persist(persist_args) {
                 });
             const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0,
                                        (F & F_NOLIGHTS) != 0>(SS, x, h.t, h.prim, sk, pf);
-            if (out == SEG_CONTINUE)
-                x.r = nr;
-            else
+            if (out != SEG_CONTINUE)
                 x.depth = 0;
+            else if constexpr (!DIRECT)
+                x.r = nr;
             pf.mark(PS_STORE);
         }
     }
@@ -1048,6 +1144,183 @@ void k_persist_sort(persist_args) {
     }
 }
 
+// ----------------------------------------------------------------------
+// fp32 fast mode (RTW_PRECISION_FP32, rtw_fast.h): the persistent form with
+// every lane's path in registers -- ray, throughput, engine, depth, sample
+// id -- and camera samples taken by idle lanes (one queue reservation per
+// wave).  Waves run independently (no block barrier in the loop), so a wave
+// leaves as soon as the queue is dry and its last path has ended.
+struct fast_args {
+    rtwf::fscene S;
+    job_t J;
+    ctrs_t* C;
+    rtwf::cam32 cam;
+};
+
+template <int F, bool LST>
+__global__ __launch_bounds__(kBlock) void k_fast(fast_args A) {
+    using namespace rtwf;
+    __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kBlock];
+    __shared__ uint32_t s_cnt[kWaves];
+    const fscene& S = A.S;
+    const uint32_t lane = threadIdx.x & 63;
+    const int own = blockIdx.x % kQShards;
+    fray r{f3{0, 0, 0}, f3{0, 0, 1}, 0};
+    f3 thr{1, 1, 1};
+    uint32_t rng = 0, depth = 0, q = 0, segs = 0;
+    bool open = true;  // wave-uniform: the queue may still hold samples
+    for (;;) {
+        // idle lanes take new camera samples (RayTracingWeekend.cpp:227-231)
+        const bool idle = depth == 0;
+        const unsigned long long m = __ballot(idle);
+        if (open && m) {
+            const uint32_t want = (uint32_t)__popcll(m);
+            const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+            uint32_t left = want, given = 0, nq = 0;
+            bool got = false;
+            for (int a = 0; a < kQShards && left; ++a) {
+                const int sh = (own + a) % kQShards;
+                const unsigned long long lim = shard_limit(sh, A.J.total);
+                unsigned long long b = ~0ull;
+                if (lane == 0) {
+                    const bool dry = a > 0 && __hip_atomic_load(&A.C->qshard[sh].v, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT) >= lim;
+                    if (!dry) b = atomicAdd(&A.C->qshard[sh].v, (unsigned long long)left);
+                }
+                b = __shfl(b, 0, 64);
+                if (b == ~0ull || b >= lim) continue;
+                const uint32_t ok = (uint32_t)min((unsigned long long)left, lim - b);
+                if (idle && rank >= given && rank < given + ok) {
+                    nq = (uint32_t)shard_sample(sh, b + (rank - given));
+                    got = true;
+                }
+                given += ok;
+                left -= ok;
+            }
+            if (left) open = false;
+            if (got) {
+                int i, j, sm;
+                sample_coords(A.J, nq, i, j, sm);
+                rng = path_seed(A.J.seed_mix, (uint32_t)(j * A.J.nx + i), (uint32_t)sm);
+                const float u = ((float)i + u01(rng)) * rcp((float)A.J.nx);
+                const float v = ((float)j + u01(rng)) * rcp((float)A.J.ny);
+                r = camera_ray(A.cam, u, v, rng);
+                thr = f3{1, 1, 1};
+                depth = (uint32_t)A.J.max_depth;
+                q = nq;
+            }
+        }
+        if (!__any(depth != 0)) break;
+        if (depth == 0) continue;
+        fhit h;
+        if constexpr (LST) {
+            lds_stackf stk{&s_stack[0][threadIdx.x]};
+            h = world_closest<F>(S, r, rng, stk);
+        } else {
+            priv_stackf stk;
+            h = world_closest<F>(S, r, rng, stk);
+        }
+        ++segs;
+        // one segment of color() (RayTracingWeekend.cpp:52-159)
+        bool end = true;
+        f3 L{0, 0, 0};
+        if (h.prim == -1) {  // background :141-159
+            if (S.background == RTW_BG_GRADIENT) {
+                const float t = 0.5f * (normalize(r.d).y + 1.0f);
+                L = thr * (f3{1, 1, 1} * (1.0f - t) + f3{0.5f, 0.7f, 1.0f} * t);
+            }
+        } else {
+            f3 p, n;
+            int mat, fp;
+            hit_record(S, r, h, p, n, mat, fp);
+            if (S.render_type == RTW_RENDER_NORMAL) {  // :135-136
+                L = thr * ((n + f3{1, 1, 1}) * 0.5f);
+            } else {
+                const mat32& M = S.materials[mat];
+                const int type = M.type;
+                if (type == RTW_MAT_DIFFUSE_LIGHT) {  // material.h:232-244, one-sided
+                    if (dot(n, r.d) > 0) L = thr * texture_value(S, M.texture, p);
+                } else {
+                    f3 f{1, 1, 1}, dir;
+                    bool alive = true;
+                    if (type == RTW_MAT_METAL) {  // material.h:128-136
+                        dir = reflect(normalize(r.d), n) + rtwf::random_in_unit_sphere(rng) * M.fuzz;
+                        f = ldf3(M.albedo);
+                    } else if (type == RTW_MAT_DIELECTRIC) {  // material.h:146-222
+                        const float dn = dot(r.d, n), il = __builtin_amdgcn_rsqf(len2(r.d));
+                        const float ri = M.ref_idx;
+                        f3 outward;
+                        float ni, cosine;
+                        if (dn > 0) {
+                            outward = -n;
+                            ni = ri;
+                            cosine = dn * il;
+                            cosine = fsqrt(__builtin_fmaxf(0.0f, 1 - ri * ri * (1 - cosine * cosine)));
+                        } else {
+                            outward = n;
+                            ni = M.inv_ref_idx;
+                            cosine = -dn * il;
+                        }
+                        const f3 uv = r.d * il;
+                        const float dt = dot(uv, outward);
+                        const float disc = 1.0f - ni * ni * (1 - dt * dt);
+                        f3 refracted{0, 0, 0};
+                        float reflect_prob = 1.0f;
+                        if (disc > 0) {
+                            refracted = (uv - outward * dt) * ni - outward * fsqrt(disc);
+                            const float x = 1 - cosine, x2 = x * x;
+                            reflect_prob = M.r0 + (1 - M.r0) * (x2 * x2 * x);
+                        }
+                        dir = u01(rng) < reflect_prob ? reflect(r.d, n) : refracted;
+                    } else if (type == RTW_MAT_ISOTROPIC) {  // material.h:257-262
+                        dir = rtwf::random_in_unit_sphere(rng);
+                        f = texture_value(S, M.texture, p);
+                    } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
+                        const onbf fr = frame(S, n, fp);
+                        float pdf_val;
+                        if (S.n_lights > 0) {
+                            dir = mixture_generate(S, fr, p, rng);
+                            const float cw = dot(normalize(dir), fr.w);
+                            pdf_val = 0.5f * (cw <= 0 ? 0.0f : cw * (1.0f / kPiF)) + 0.5f * lights_pdf_value(S, p, dir);
+                        } else {
+                            const float r1 = u01(rng), r2 = u01(rng);
+                            dir = local(fr, cone_dir(r1, fsqrt(1 - r2)));
+                            const float cw = dot(normalize(dir), fr.w);
+                            pdf_val = cw <= 0 ? 0.0f : cw * (1.0f / kPiF);
+                        }
+                        if (pdf_val > 0) {
+                            const float cosine = dot(n, normalize(dir));
+                            const float spdf = cosine < 0 ? 0.0f : cosine * (1.0f / kPiF);
+                            f = texture_value(S, M.texture, p) * (spdf * rcp(pdf_val));
+                        } else {
+                            alive = false;  // :126-127 returns emitted (0)
+                        }
+                    }
+                    if (alive && depth > 1) {  // the next color() call has depth - 1
+                        thr = thr * f;
+                        r = fray{p, dir, r.t};
+                        --depth;
+                        end = false;
+                    }
+                }
+            }
+        }
+        if (end) {
+            double* o = A.J.L + 3 * (size_t)q;
+            o[0] = (double)L.x, o[1] = (double)L.y, o[2] = (double)L.z;
+            depth = 0;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_down(segs, off, 64);
+    if (lane == 0) s_cnt[threadIdx.x >> 6] = segs;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int k = 0; k < kWaves; ++k) t += s_cnt[k];
+        if (t) atomicAdd(&A.C->segments[blockIdx.x % 8].v, t);
+    }
+}
+
 // Block-wide exclusive prefix sum of one value per thread (blockDim = kBlock).
 __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1181,7 +1454,50 @@ __global__ void k_commit(ctrs_t* C) {
     C->n_out = 0;
 }
 
-// running[pix] += L[s][pix] for s = 0..S-1 in order (RayTracingWeekend.cpp:235-239)
+// running[pix] += sample s of pix for s = 0..S-1 in order (RayTracingWeekend.cpp:235-239)
+#if RTW_PIXEL_MAJOR
+// Pixel-major records: a block takes 64 consecutive pixels, whose records
+// are one contiguous run, and streams it through LDS in chunks of kRedChunk
+// samples (coalesced loads of each pixel's contiguous 24 * kRedChunk bytes);
+// thread 3k + c then adds channel c of pixel k's chunk in sample order.
+constexpr uint32_t kRedPix = 64, kRedChunk = 16;
+__global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ L, uint32_t npix, uint32_t spp,
+                                                   double* __restrict__ run) {
+    // one pixel's chunk per row, rows padded to an odd number of doubles so
+    // the summing threads' reads (3 per pixel, one row apart) spread over
+    // the LDS banks
+    constexpr uint32_t kRow = 3 * kRedChunk + 1;
+    __shared__ double s_rec[kRedPix * kRow];  // 24.5 KB
+    for (uint32_t p0 = blockIdx.x * kRedPix; p0 < npix; p0 += gridDim.x * kRedPix) {
+        const uint32_t np = min(kRedPix, npix - p0);
+        const uint32_t me = threadIdx.x;
+        const bool summer = me < 3 * np;
+        double acc = summer ? run[3 * (size_t)p0 + me] : 0.0;
+        for (uint32_t s0 = 0; s0 < spp; s0 += kRedChunk) {
+            const uint32_t cs = min(kRedChunk, spp - s0), row = 3 * cs;
+            __syncthreads();  // the previous chunk has been summed
+            if (cs == kRedChunk && np == kRedPix) {  // full chunk: constant shapes
+#pragma unroll
+                for (uint32_t k = me; k < kRedPix * 3 * kRedChunk; k += kBlock) {
+                    const uint32_t pk = k / (3 * kRedChunk), o = k - pk * (3 * kRedChunk);
+                    s_rec[pk * kRow + o] = L[3 * ((size_t)(p0 + pk) * spp + s0) + o];
+                }
+            } else {
+                for (uint32_t k = me; k < np * row; k += kBlock) {
+                    const uint32_t pk = k / row, o = k - pk * row;
+                    s_rec[pk * kRow + o] = L[3 * ((size_t)(p0 + pk) * spp + s0) + o];
+                }
+            }
+            __syncthreads();
+            if (summer) {
+                const uint32_t pk = me / 3, c = me - 3 * pk;
+                for (uint32_t s = 0; s < cs; ++s) acc = acc + s_rec[pk * kRow + 3 * s + c];
+            }
+        }
+        if (summer) run[3 * (size_t)p0 + me] = acc;
+    }
+}
+#else
 __global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ L, uint32_t npix, uint32_t spp,
                                                    double* __restrict__ run) {
     for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < npix; p += gridDim.x * kBlock) {
@@ -1194,6 +1510,15 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ L,
         }
         run[3 * p] = r, run[3 * p + 1] = g, run[3 * p + 2] = bl;
     }
+}
+#endif
+// k_reduce's grid for npix pixels
+unsigned reduce_grid(uint64_t npix) {
+#if RTW_PIXEL_MAJOR
+    return (unsigned)std::min<uint64_t>((npix + kRedPix - 1) / kRedPix, 8192);
+#else
+    return (unsigned)std::min<uint64_t>((npix + kBlock - 1) / kBlock, 4096);
+#endif
 }
 
 // accum[(j*nx+i)*3+c] += run[(k*nx+i)*3+c], j = row_begin + k*row_step
@@ -1266,6 +1591,8 @@ struct handle_t {
     const char* scene_base = nullptr;
     uint32_t shade_bytes = 0;  // bytes of the shading prefix of scene_mem
     dev_buf scene_mem;
+    dev_buf scene32;  // fp32 mirror of the scene (fast mode, rtw_fast.h)
+    rtwf::fscene F32{};
     dev_buf pool[2];  // path SoA, ping-pong for compaction
     dev_buf fresh;    // staging of new camera rays (fresh_t)
     dev_buf hits;
@@ -1734,6 +2061,107 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     if (h->stack_need > kStack)
         return rtw_fail(RTW_ERR_UNSUPPORTED, "BVH too deep for the traversal stack (" + std::to_string(h->stack_need) +
                                                  " > " + std::to_string(kStack) + " entries)");
+
+    // fp32 mirror for the fast mode (rtw_fast.h): prims, entries, ops,
+    // materials, textures, Perlin vectors and rect frames in single
+    // precision; BVH nodes / items, world runs, the media walk and the lights
+    // are the arrays above
+    {
+        using namespace rtwf;
+        std::vector<prim32> p32(std::max(d->n_prims, 1));
+        for (int i = 0; i < d->n_prims; ++i) {
+            const rtw_prim& q = d->prims[i];
+            prim32& o = p32[i];
+            std::memset(&o, 0, sizeof o);
+            o.type = q.type, o.material = q.material, o.flip = q.flip, o.entry = q.entry;
+            for (int k = 0; k < 10; ++k) o.p[k] = (float)q.p[k];
+            if (is_sphere(q.type)) {
+                o.p[9] = (float)(q.p[3] * q.p[3]);
+                if (q.type == RTW_PRIM_MOVING_SPHERE) {
+                    for (int k = 0; k < 3; ++k) o.p[4 + k] = (float)(q.p[4 + k] - q.p[k]);
+                    o.p[7] = (float)q.p[7];
+                    o.p[8] = (float)(1.0 / (q.p[8] - q.p[7]));
+                }
+            }
+        }
+        std::vector<ent32> e32(std::max(d->n_entries, 1));
+        for (int e = 0; e < d->n_entries; ++e) {
+            const dev_entry& D = dev_entries[e];
+            ent32& o = e32[e];
+            std::memset(&o, 0, sizeof o);
+            o.kind = D.kind, o.first_prim = D.first_prim, o.n_prims = D.n_prims, o.n_ops = D.n_ops;
+            o.first_op = D.first_op, o.phase_material = D.phase_material;
+            o.bvh_root = bvh_ok ? D.bvh_root : -1;
+            o.n_outer_ops = D.n_outer_ops;
+            o.neg_inv_density = (float)(-(1.0 / D.density));
+        }
+        std::vector<op32> o32(std::max<size_t>(dev_ops.size(), 1));
+        for (size_t k = 0; k < dev_ops.size(); ++k) {
+            o32[k].type = dev_ops[k].type;
+            for (int j = 0; j < 3; ++j) o32[k].p[j] = (float)dev_ops[k].p[j];
+        }
+        std::vector<mat32> m32(std::max(d->n_materials, 1));
+        for (int k = 0; k < d->n_materials; ++k) {
+            const rtw_material& M = d->materials[k];
+            mat32& o = m32[k];
+            std::memset(&o, 0, sizeof o);
+            o.type = M.type, o.texture = M.texture;
+            for (int j = 0; j < 3; ++j) o.albedo[j] = (float)M.albedo[j];
+            o.fuzz = (float)M.fuzz, o.ref_idx = (float)M.ref_idx;
+            o.inv_ref_idx = (float)mat_aux[2 * k], o.r0 = (float)mat_aux[2 * k + 1];
+        }
+        std::vector<tex32> t32(std::max(d->n_textures, 1));
+        for (int k = 0; k < d->n_textures; ++k) {
+            const rtw_texture& T = d->textures[k];
+            tex32& o = t32[k];
+            std::memset(&o, 0, sizeof o);
+            o.type = T.type, o.odd = T.odd, o.even = T.even, o.scale = (float)T.scale;
+            for (int j = 0; j < 3; ++j) o.color[j] = (float)T.color[j];
+        }
+        std::vector<float> rv32(768, 0.0f), fr32(frames.size());
+        if (d->has_perlin)
+            for (int k = 0; k < 768; ++k) rv32[k] = (float)d->perlin_ranvec[k];
+        for (size_t k = 0; k < frames.size(); ++k) fr32[k] = (float)frames[k];
+        std::vector<part> p2 = {
+            {p32.data(), sizeof(prim32) * p32.size(), 0},   {e32.data(), sizeof(ent32) * e32.size(), 0},
+            {o32.data(), sizeof(op32) * o32.size(), 0},     {m32.data(), sizeof(mat32) * m32.size(), 0},
+            {t32.data(), sizeof(tex32) * t32.size(), 0},    {rv32.data(), sizeof(float) * rv32.size(), 0},
+            {fr32.data(), sizeof(float) * fr32.size(), 0},
+        };
+        size_t tot = 0;
+        for (auto& x : p2) {
+            x.off = tot;
+            tot += (x.bytes + 255) & ~size_t(255);
+        }
+        if ((rc = h->scene32.ensure(std::max<size_t>(tot, 256)))) return rc;
+        std::vector<char> st2(std::max<size_t>(tot, 256), 0);
+        for (auto& x : p2)
+            if (x.bytes) std::memcpy(st2.data() + x.off, x.src, x.bytes);
+        HIPCHK(hipMemcpy(h->scene32.p, st2.data(), st2.size(), hipMemcpyHostToDevice));
+        char* b2 = static_cast<char*>(h->scene32.p);
+        fscene& F = h->F32;
+        F.prims = (const prim32*)(b2 + p2[0].off);
+        F.entries = (const ent32*)(b2 + p2[1].off);
+        F.ops = (const op32*)(b2 + p2[2].off);
+        F.materials = (const mat32*)(b2 + p2[3].off);
+        F.textures = (const tex32*)(b2 + p2[4].off);
+        F.ranvec = (const float*)(b2 + p2[5].off);
+        F.frames = (const float*)(b2 + p2[6].off);
+        F.lights = S.lights;
+        F.perm = S.perm;
+        F.nodes = S.nodes;
+        F.items = S.items;
+        F.runs = S.runs;
+        F.media = S.media;
+        F.light_weight = (float)S.light_weight;
+        F.n_lights = S.n_lights;
+        F.world_bvh_root = S.world_bvh_root;
+        F.render_type = S.render_type;
+        F.background = S.background;
+        F.n_media = S.n_media;
+        F.n_runs = S.n_runs;
+        F.n_nodes = S.n_nodes;
+    }
     return RTW_OK;
 }
 
@@ -1950,6 +2378,38 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     return false;
 }
 
+// The fp32 fast-mode kernel of a scene: one instantiation per traversal
+// feature set, LDS stacks when the deepest walk fits them.  grid = resident
+// blocks (occupancy query, cached).  probe: name it only.
+template <int FF, bool LST>
+void launch_fast_t(bool probe, std::string* name, int cus, hipStream_t st, const fast_args& A) {
+    if (name) *name = kname("k_fast", FF, -1, LST ? 1 : 0);
+    if (probe) return;
+    const int grid = blocks_per_cu(reinterpret_cast<const void*>(&k_fast<FF, LST>), kBlock, 0) * cus;
+    hipLaunchKernelGGL((k_fast<FF, LST>), dim3(grid), dim3(kBlock), 0, st, A);
+}
+void launch_fast(bool probe, const handle_t* h, hipStream_t st, const fast_args& A, std::string* name = nullptr) {
+    const int f = h->features & (F_MEDIA | F_WBVH | F_GBVH);
+    const bool lst = (f & (F_WBVH | F_GBVH)) && h->stack_need <= kLdsStack && h->S.n_nodes < 65536;
+    switch (f * 2 + (lst ? 1 : 0)) {
+#define RTW_FAST(FF, LL) \
+    case (FF) * 2 + (LL ? 1 : 0): launch_fast_t<FF, LL>(probe, name, h->cus, st, A); break;
+        RTW_FAST(0, false)
+        RTW_FAST(F_MEDIA, false)
+        RTW_FAST(F_GBVH, false)
+        RTW_FAST(F_GBVH, true)
+        RTW_FAST(F_WBVH, false)
+        RTW_FAST(F_WBVH, true)
+        RTW_FAST(F_WBVH | F_GBVH, false)
+        RTW_FAST(F_WBVH | F_GBVH, true)
+        RTW_FAST(F_MEDIA | F_GBVH, false)
+        RTW_FAST(F_MEDIA | F_GBVH, true)
+#undef RTW_FAST
+    default:
+        launch_fast_t<F_MEDIA | F_GBVH, false>(probe, name, h->cus, st, A);
+    }
+}
+
 void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_t& J, const paths_t& A,
                   const fresh_t& F, const double* ht, const int32_t* hid, ctrs_t* C, const char* base, uint32_t bytes) {
     const int pick = pick_shade_mask(mask);
@@ -2081,7 +2541,7 @@ int validate_desc(const rtw_scene_desc* d) {
     // prims of the entry's own range (group BVH) or entry indices (world).
     {
         std::vector<int> seen(d->n_bvh_nodes, 0);
-        auto walk = [&](int root, int lo, int hi, const char* what) -> int {
+        auto walk = [&](int root, int lo, int hi, const char* what, bool group_items) -> int {
             std::vector<int> todo{root};
             while (!todo.empty()) {
                 const int n = todo.back();
@@ -2093,19 +2553,34 @@ int validate_desc(const rtw_scene_desc* d) {
                     todo.push_back(N.right);
                     continue;
                 }
-                for (int k = N.left; k < N.left + N.count; ++k)
-                    if (d->bvh_items[k] < lo || d->bvh_items[k] >= hi)
+                for (int k = N.left; k < N.left + N.count; ++k) {
+                    int it = d->bvh_items[k], span = 1;
+                    if (!group_items && it < 0)
                         return rtw_fail(RTW_ERR_INVALID, std::string(what) + " BVH item out of range");
+                    if (group_items && it >= 0 && (it & RTW_ITEM_BOX)) {  // a box: six rects in box order
+                        it &= RTW_ITEM_INDEX;
+                        span = 6;
+                        static const int kBoxTypes[6] = {RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XZ,
+                                                         RTW_PRIM_RECT_XZ, RTW_PRIM_RECT_YZ, RTW_PRIM_RECT_YZ};
+                        if (it >= lo && it + 6 <= hi)
+                            for (int j = 0; j < 6; ++j)
+                                if (d->prims[it + j].type != kBoxTypes[j])
+                                    return rtw_fail(RTW_ERR_INVALID, "box item " + std::to_string(k) +
+                                                                         ": its prims are not a box's six rects");
+                    }
+                    if (it < lo || it + span > hi)
+                        return rtw_fail(RTW_ERR_INVALID, std::string(what) + " BVH item out of range");
+                }
             }
             return RTW_OK;
         };
         for (int e = 0; e < d->n_entries; ++e) {
             const rtw_entry& E = d->entries[e];
             if (E.bvh_root < 0) continue;
-            if (int rc = walk(E.bvh_root, E.first_prim, E.first_prim + E.n_prims, "group")) return rc;
+            if (int rc = walk(E.bvh_root, E.first_prim, E.first_prim + E.n_prims, "group", true)) return rc;
         }
         if (d->world_bvh_root >= 0)
-            if (int rc = walk(d->world_bvh_root, 0, d->n_entries, "world")) return rc;
+            if (int rc = walk(d->world_bvh_root, 0, d->n_entries, "world", false)) return rc;
     }
     return RTW_OK;
 }
@@ -2191,6 +2666,9 @@ extern "C" int rtw_scene_query(void* handle, rtw_scene_info* out) {
     out->bvh_lds_nodes = (int32_t)g_node_packet;  // set by the probe (launch_pk)
     std::snprintf(out->kernel, sizeof out->kernel, "%s", k.c_str());
     std::snprintf(out->build_id, sizeof out->build_id, "%s", RTW_BUILD_ID);
+    std::string kf;
+    launch_fast(true, h, nullptr, fast_args{}, &kf);
+    std::snprintf(out->kernel_fast, sizeof out->kernel_fast, "%s", kf.c_str());
     return RTW_OK;
 }
 
@@ -2278,6 +2756,7 @@ extern "C" void rtw_scene_free(void* handle) {
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     h->scene_mem.release();
+    h->scene32.release();
     h->pool[0].release();
     h->pool[1].release();
     h->fresh.release();
@@ -2402,14 +2881,33 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     // execution form: persistent (paths in registers, one launch per pass)
     // unless RTW_MODE=wavefront or no persistent instantiation covers the scene
     const char* mode_env = std::getenv("RTW_MODE");
-    const bool persistent = !(mode_env && std::string(mode_env) == "wavefront") &&
-                            launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J, C, h->scene_base,
-                                           h->shade_bytes, h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0,
-                                           h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL);
+    // fp32 fast mode: its own persistent kernel (rtw_fast.h), same passes,
+    // radiance records and ordered per-pixel reduction
+    const bool fast = R.precision == RTW_PRECISION_FP32;
+    fast_args FA{};
+    if (fast) {
+        FA.S = h->F32;
+        FA.C = C;
+        const rtw_camera_desc& c = *camera;
+        for (int k = 0; k < 3; ++k) {
+            FA.cam.origin[k] = (float)c.origin[k], FA.cam.lower_left[k] = (float)c.lower_left[k];
+            FA.cam.horizontal[k] = (float)c.horizontal[k], FA.cam.vertical[k] = (float)c.vertical[k];
+            FA.cam.u[k] = (float)c.u[k], FA.cam.v[k] = (float)c.v[k];
+        }
+        FA.cam.time0 = (float)c.time0, FA.cam.dtime = (float)(c.time1 - c.time0);
+        FA.cam.lens_radius = (float)c.lens_radius;
+    }
+    const bool persistent = fast || (!(mode_env && std::string(mode_env) == "wavefront") &&
+                                     launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J, C,
+                                                    h->scene_base, h->shade_bytes, h->stack_need, h->ysph, !h->movers,
+                                                    h->S.n_lights > 0,
+                                                    h->S.background != RTW_BG_GRADIENT &&
+                                                        h->S.render_type != RTW_RENDER_NORMAL));
 
     for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
         J.total = (uint32_t)(S_pass * npix);
+        J.spp_pass = S_pass;
         J.s_begin = R.spp_begin + (int)done;
         const uint32_t n0 = std::min<uint32_t>(pool, J.total);
         if (persistent) {
@@ -2420,9 +2918,14 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
                 HIPCHK(hipEventRecord(h->events[e0], st));
             }
-            launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base, h->shade_bytes,
-                           h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0,
-                                           h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL);
+            if (fast) {
+                FA.J = J;
+                launch_fast(false, h, st, FA);
+            } else {
+                launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base,
+                               h->shade_bytes, h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0,
+                               h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL);
+            }
             HIPCHK(hipGetLastError());
             if (timed) {
                 HIPCHK(hipEventRecord(h->events[e1], st));
@@ -2430,7 +2933,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
             }
             stats.launches_intersect++;
             stats.iterations++;
-            hipLaunchKernelGGL(k_reduce, dim3(std::min<uint64_t>((npix + kBlock - 1) / kBlock, 4096)), dim3(kBlock), 0,
+            hipLaunchKernelGGL(k_reduce, dim3(reduce_grid(npix)), dim3(kBlock), 0,
                                st, J.L, (uint32_t)npix, S_pass, run);
             HIPCHK(hipGetLastError());
             stats.samples += J.total;
@@ -2510,7 +3013,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 if (tail && snap.n == 0) break;
             }
         }
-        hipLaunchKernelGGL(k_reduce, dim3(std::min<uint64_t>((npix + kBlock - 1) / kBlock, 4096)), dim3(kBlock), 0, st,
+        hipLaunchKernelGGL(k_reduce, dim3(reduce_grid(npix)), dim3(kBlock), 0, st,
                            J.L, (uint32_t)npix, S_pass, run);
         HIPCHK(hipGetLastError());
         stats.samples += J.total;
@@ -2592,7 +3095,8 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     // algorithmic traversal bytes: 56 B ray in +
     // 12 B hit out per world query, whatever the execution form (k_persist
     // keeps both in registers; k_segment / k_intersect stream them)
-    stats.bytes_intersect = 68.0 * (double)stats.segments;
+    // (fp32 fast mode: 7 x 4 B ray in, 4 + 4 B hit out = 36 B)
+    stats.bytes_intersect = (fast ? 36.0 : 68.0) * (double)stats.segments;
     if (out_stats) *out_stats = stats;
     return RTW_OK;
 }

@@ -169,8 +169,20 @@ def test_bvh_build_is_well_formed(render_mod):
             if tag == "world":
                 assert sorted(seen) == list(range(n))
             else:
+                # box items (RTW_ITEM_BOX | i) stand for the six rects [i, i+6)
                 e = d.entries[tag]
-                assert sorted(seen) == list(range(e.first_prim, e.first_prim + e.n_prims))
+                prims = []
+                for it in seen:
+                    if it & _abi.RTW_ITEM_BOX:
+                        i = it & _abi.RTW_ITEM_INDEX
+                        assert [d.prims[i + j].type for j in range(6)] == [_abi.RTW_PRIM_RECT_XY] * 2 + \
+                            [_abi.RTW_PRIM_RECT_XZ] * 2 + [_abi.RTW_PRIM_RECT_YZ] * 2
+                        prims += range(i, i + 6)
+                    else:
+                        prims.append(it)
+                assert sorted(prims) == list(range(e.first_prim, e.first_prim + e.n_prims))
+                if name == "book2_final" and e.n_prims == 2400:  # the 400 ground boxes
+                    assert sum(1 for it in seen if it & _abi.RTW_ITEM_BOX) == 400
 
 
 def test_unknown_scene_is_an_error(render_mod):
