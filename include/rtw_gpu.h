@@ -24,7 +24,9 @@
  *   - calls are thread-compatible: one render per scene handle at a time.
  *
  * Arithmetic is IEEE fp64 throughout (the reference computes in double,
- * vec3.h:35-44).  Randomness: every camera sample owns one std::minstd_rand
+ * vec3.h:35-44), unless a render asks for the fp32 fast mode
+ * (rtw_render_params.precision = RTW_PRECISION_FP32: statistical parity
+ * only).  Randomness: every camera sample owns one std::minstd_rand
  * stream (48271 * x mod 2^31-1, libstdc++ generate_canonical<double,53>, i.e.
  * two raw draws per double) seeded from (seed, pixel, sample) by
  * rtw_path_seed() below, so results do not depend on how samples are sharded

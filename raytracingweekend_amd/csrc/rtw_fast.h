@@ -108,7 +108,9 @@ struct fscene {
     const int32_t* items;
     const world_run* runs;
     const int32_t* media;
+    const float* ysph;  // the y-sphere runs' pair-interleaved fp32 records (rtw_scene_upload)
     float light_weight;
+    float mv_t0, mv_inv_den;  // the common motion interval of the y-sphere runs' movers
     int32_t n_lights, world_bvh_root, render_type, background, n_media, n_runs, n_nodes;
 };
 
@@ -251,6 +253,47 @@ RTW_D void group_scan(const fscene& S, int first, int n, const fray& r, float tm
         } else {
             if (rect_t(q, r, tmin, h.t, t)) h.t = t, h.prim = i, h.rect = true;
         }
+    }
+}
+
+// A y-sphere run (WORLD_RUN_YSPHERES: spheres moving along y at most, the
+// Book-1 random_balls list): the discriminants of two spheres per packed
+// fp32 instruction (v_pk_fma_f32) from the upload's pair-interleaved records
+// {cx, cy, cz, dy, r^2}, and the full test -- list order, strict t < t_max
+// only for spheres some lane of the wave may hit.  fc = the walk's motion
+// fraction.  Spheres the records do not bound (r^2 = +inf: the ground) always
+// pass to the full test.
+RTW_D void ysphere_scan(const fscene& S, int first, int n, const fray& r, float tmin, fhit& h, float fc) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const float a = dot(r.d, r.d);
+    auto full = [&](int i) {
+        const prim32 q = uprim(S.prims, first + i);
+        float t;
+        if (sphere_t(q, r, tmin, h.t, t)) h.t = t, h.prim = first + i, h.rect = false;
+    };
+    const f2 ox2 = r.o.x, oy2 = r.o.y, oz2 = r.o.z, dx2 = r.d.x, dy2 = r.d.y, dz2 = r.d.z, fc2 = fc, a2 = a;
+    auto disc = [&](f2 cx, f2 cy, f2 cz, f2 dy, f2 rr, f2& slack) {
+        const f2 ocx = ox2 - cx, ocz = oz2 - cz;
+        const f2 ocy = __builtin_elementwise_fma(-dy, fc2, oy2 - cy);
+        const f2 b = __builtin_elementwise_fma(ocx, dx2, __builtin_elementwise_fma(ocy, dy2, ocz * dz2));
+        const f2 q = __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz));
+        slack = 0x1p-18f * a2 * (q + rr);  // the filter's own rounding, generously
+        return __builtin_elementwise_fma(b, b, -(a2 * (q - rr)));
+    };
+    const f2* g0 = reinterpret_cast<const f2*>(S.ysph + 8 * (size_t)first);
+    const int np = n >> 1;
+    for (int p = 0; p < np; ++p) {
+        const f2* g = g0 + 8 * p;
+        f2 e;
+        const f2 d = disc(ld(g), ld(g + 1), ld(g + 2), ld(g + 3), ld(g + 4), e);
+        if (__builtin_amdgcn_ballot_w64(!(d.x <= -e.x))) full(2 * p);
+        if (__builtin_amdgcn_ballot_w64(!(d.y <= -e.y))) full(2 * p + 1);
+    }
+    if (n & 1) {  // the last sphere of an odd run keeps a plain record
+        const float* g = S.ysph + 8 * (size_t)(first + n - 1);
+        f2 e;
+        const f2 d = disc(f2(ld(g)), f2(ld(g + 1)), f2(ld(g + 2)), f2(ld(g + 3)), f2(ld(g + 4)), e);
+        if (__builtin_amdgcn_ballot_w64(!(d.x <= -e.x))) full(n - 1);
     }
 }
 
@@ -421,6 +464,11 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
     } else {
         for (int ri = 0; ri < S.n_runs; ++ri) {
             const int ei = ld(&S.runs[ri].entry);
+            if (ei == rtwd::WORLD_RUN_YSPHERES) {
+                const float fc = ld(&S.runs[ri].movers) ? (r.t - S.mv_t0) * S.mv_inv_den : 0.0f;
+                ysphere_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), r, kTMinF, h, fc);
+                continue;
+            }
             fray lr = r;
             if (ei >= 0) {
                 const ent_v e = view_entry<true>(S, ei);
@@ -587,6 +635,109 @@ RTW_D float lights_pdf_value(const fscene& S, f3 o, f3 v) {  // hittable_list.h:
 }
 
 RTW_D f3 reflect(f3 v, f3 n) { return v - n * (2.0f * dot(v, n)); }  // material.h:10-13
+
+// ------------------------------------------------------------------ shading
+// One segment of color() (RayTracingWeekend.cpp:52-159) for a path whose
+// world hit is h: the path ends with radiance thr * w (emission or
+// background; w = 0 for an absorbed path), or continues with thr *= w along
+// `next` (depth - 1).  rng advances by the draws the branch takes.
+struct seg_f {
+    bool cont;
+    f3 w;
+    fray next;
+};
+RTW_D seg_f shade(const fscene& S, const fray& r, const fhit& h, uint32_t& rng, uint32_t depth) {
+    seg_f o{false, f3{0, 0, 0}, r};
+    if (h.prim == -1) {  // background :141-159
+        if (S.background == RTW_BG_GRADIENT) {
+            const float t = 0.5f * (normalize(r.d).y + 1.0f);
+            o.w = f3{1, 1, 1} * (1.0f - t) + f3{0.5f, 0.7f, 1.0f} * t;
+        }
+        return o;
+    }
+    f3 p, n;
+    int mat, fp;
+    hit_record(S, r, h, p, n, mat, fp);
+    if (S.render_type == RTW_RENDER_NORMAL) {  // :135-136
+        o.w = (n + f3{1, 1, 1}) * 0.5f;
+        return o;
+    }
+    const mat32& M = S.materials[mat];
+    const int type = M.type;
+    if (type == RTW_MAT_DIFFUSE_LIGHT) {  // material.h:232-244, one-sided
+        if (dot(n, r.d) > 0) o.w = texture_value(S, M.texture, p);
+        return o;
+    }
+    f3 f{1, 1, 1}, dir;
+    if (type == RTW_MAT_METAL) {  // material.h:128-136
+        dir = reflect(normalize(r.d), n) + random_in_unit_sphere(rng) * M.fuzz;
+        f = ldf3(M.albedo);
+    } else if (type == RTW_MAT_DIELECTRIC) {  // material.h:146-222
+        const float dn = dot(r.d, n), il = __builtin_amdgcn_rsqf(len2(r.d));
+        const float ri = M.ref_idx;
+        f3 outward;
+        float ni, cosine;
+        if (dn > 0) {
+            outward = -n;
+            ni = ri;
+            cosine = dn * il;
+            cosine = fsqrt(__builtin_fmaxf(0.0f, 1 - ri * ri * (1 - cosine * cosine)));
+        } else {
+            outward = n;
+            ni = M.inv_ref_idx;
+            cosine = -dn * il;
+        }
+        const f3 uv = r.d * il;
+        const float dt = dot(uv, outward);
+        const float disc = 1.0f - ni * ni * (1 - dt * dt);
+        f3 refracted{0, 0, 0};
+        float reflect_prob = 1.0f;
+        if (disc > 0) {
+            refracted = (uv - outward * dt) * ni - outward * fsqrt(disc);
+            const float x = 1 - cosine, x2 = x * x;
+            reflect_prob = M.r0 + (1 - M.r0) * (x2 * x2 * x);
+        }
+        dir = u01(rng) < reflect_prob ? reflect(r.d, n) : refracted;
+    } else if (type == RTW_MAT_ISOTROPIC) {  // material.h:257-262
+        dir = random_in_unit_sphere(rng);
+        f = texture_value(S, M.texture, p);
+    } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
+        const onbf fr = frame(S, n, fp);
+        float pdf_val;
+        if (S.n_lights > 0) {
+            dir = mixture_generate(S, fr, p, rng);
+            const float cw = dot(normalize(dir), fr.w);
+            pdf_val = 0.5f * (cw <= 0 ? 0.0f : cw * (1.0f / kPiF)) + 0.5f * lights_pdf_value(S, p, dir);
+        } else {
+            const float r1 = u01(rng), r2 = u01(rng);
+            dir = local(fr, cone_dir(r1, fsqrt(1 - r2)));
+            const float cw = dot(normalize(dir), fr.w);
+            pdf_val = cw <= 0 ? 0.0f : cw * (1.0f / kPiF);
+        }
+        if (!(pdf_val > 0)) return o;  // :126-127 returns emitted (0)
+        const float cosine = dot(n, normalize(dir));
+        const float spdf = cosine < 0 ? 0.0f : cosine * (1.0f / kPiF);
+        f = texture_value(S, M.texture, p) * (spdf * rcp(pdf_val));
+    }
+    if (depth <= 1) return o;  // the next color() call has depth 0: returns 0
+    o.cont = true;
+    o.w = f;
+    o.next = fray{p, dir, r.t};
+    return o;
+}
+
+// the material class of a hit, the key the regrouping kernel sorts by
+enum { FK_LAMB = 0, FK_DIEL, FK_METAL, FK_ISO, FK_EMIT, FK_MISS, FK_IDLE, FK_N };
+RTW_D int hit_key(const fscene& S, const fhit& h) {
+    if (h.prim == -1) return FK_MISS;
+    const int mat = h.prim <= -2 ? S.entries[-h.prim - 2].phase_material : S.prims[h.prim].material;
+    const int ty = S.materials[mat].type;
+    return ty == RTW_MAT_LAMBERTIAN ? FK_LAMB
+           : ty == RTW_MAT_DIELECTRIC ? FK_DIEL
+           : ty == RTW_MAT_METAL ? FK_METAL
+           : ty == RTW_MAT_ISOTROPIC ? FK_ISO
+                                     : FK_EMIT;
+}
 
 // ------------------------------------------------------------------ camera
 struct cam32 {

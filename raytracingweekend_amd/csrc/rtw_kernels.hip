@@ -105,16 +105,19 @@ struct job_t {
     double* L;           // per-sample radiance, L[3q + c] (pass-local sample id q)
 };
 
-// Pass-local sample ids are pixel-major (RTW_PIXEL_MAJOR): q = pixel *
-// spp_pass + sample, so the 64 ids a wave reserves are 64 samples of one
-// pixel and their 24-byte radiance records fill whole cache lines of one
-// contiguous 1.5 KB run (sample-major ids scattered them over 64 pixels'
-// planes: partial-sector writes, 1.55x the record bytes); k_reduce then
-// reads each pixel's records as one contiguous run.  Results do not depend
-// on it: the RNG is keyed by (pixel, sample) and each pixel's records are
-// still summed in increasing sample order.
+// Pass-local sample ids are sample-major: q = sample * npix + pixel, so a
+// wave's 64 consecutive ids are 64 neighbouring pixels and k_reduce reads
+// each sample plane coalesced.  RTW_PIXEL_MAJOR=1 makes them pixel-major
+// (q = pixel * spp_pass + sample): a wave's 64 radiance records then fill
+// whole lines of one contiguous 1.5 KB run instead of partial sectors of 64
+// pixels' planes (1.55x the record bytes), but k_reduce has to stage each
+// pixel's run through LDS to sum it in sample order.  Measured on T (1
+// MI355X, rocprofv3): traversal kernel 148.99 vs 149.12 ms, k_reduce 3.75 vs
+// 2.66 ms, the whole step -0.5 % (profiles/r03/ab_pixel_major.log) -- so
+// sample-major stays.  Results do not depend on it: the RNG is keyed by
+// (pixel, sample) and each pixel's records are summed in sample order.
 #ifndef RTW_PIXEL_MAJOR
-#define RTW_PIXEL_MAJOR 1
+#define RTW_PIXEL_MAJOR 0
 #endif
 
 // pass-local sample id -> pixel (i, j) and global sample index s
@@ -687,6 +690,11 @@ __device__ __forceinline__ const persist_args& args_now() {
 // live in registers across the walk), and the continuation written there.
 // In registers that loop-carried ray was what the Book-2 kernel spilled to
 // scratch (9 VGPRs, 48 bytes per lane, most of its HBM write traffic).
+// BIN (RTW_BIN_RAYS): wave-level binning of rays by direction octant before
+// each world-BVH walk (A/B for the divergent random_balls BVH walks).
+#ifndef RTW_BIN_RAYS
+#define RTW_BIN_RAYS(F) 0
+#endif
 // Measured (1 MI355X, A/B): C5 slice 577 vs 617 Msamples/s, C3 2617 vs
 // 2711 -- the lane-partial camera sampling costs more than the spills it
 // removes, so it is off (-DRTW_PERSIST_DIRECT(F)=1 selects it).
@@ -697,6 +705,7 @@ template <int F, int M, bool LDS, bool LST = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist(persist_args) {
     constexpr bool DIRECT = RTW_PERSIST_DIRECT(F);
+    constexpr bool BIN = RTW_BIN_RAYS(F) && !DIRECT;
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kWaves];
     __shared__ ray_batch s_batch[DIRECT ? 1 : kWaves];
@@ -722,6 +731,7 @@ void k_persist(persist_args) {
     const int own = blockIdx.x % kQShards;
     path_st x;
     x.depth = 0;
+    uint32_t home = threadIdx.x;  // BIN: the LDS slot (sample id, throughput) of this lane's path
     bool open = true;      // wave-uniform: the queue may still hold samples
     uint32_t bl = 0, bh = 0;  // wave-uniform: unread batch entries [bl, bh)
     uint32_t segs = 0;
@@ -837,8 +847,9 @@ void k_persist(persist_args) {
                     const uint32_t k = bl + rank;
                     x.r = ray{d3{B.ox[k], B.oy[k], B.oz[k]}, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
                     x.rng = B.rng[k];
-                    s_q[tid] = B.q[k];
-                    s_thr[0][tid] = 1.0, s_thr[1][tid] = 1.0, s_thr[2][tid] = 1.0;
+                    const uint32_t hm = BIN ? home : tid;
+                    s_q[hm] = B.q[k];
+                    s_thr[0][hm] = 1.0, s_thr[1][hm] = 1.0, s_thr[2][hm] = 1.0;
                     x.depth = (uint32_t)args_now().J.max_depth;
                 }
                 bl += min((uint32_t)__popcll(m), avail);
@@ -846,6 +857,34 @@ void k_persist(persist_args) {
             }
         }
         if (!__any(x.depth != 0)) break;
+        if constexpr (BIN) {
+            // wave-level binning of the paths by direction octant before the
+            // walk (live paths by octant, idle lanes last): a counting sort
+            // over ballots, then every lane's path state -- ray, engine,
+            // depth, home slot -- is pushed to the lane of its rank
+            // (ds_permute, no LDS allocation, no block barrier)
+            const int key = x.depth == 0 ? 8 : (x.r.d.x < 0 ? 1 : 0) | (x.r.d.y < 0 ? 2 : 0) | (x.r.d.z < 0 ? 4 : 0);
+            uint32_t dst = 0, before = 0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const unsigned long long m = __ballot(key == k);
+                if (key == k) dst = before + (uint32_t)__popcll(m & lanemask_lt());
+                before += (uint32_t)__popcll(m);
+            }
+            const int addr = (int)(dst * 4);
+            auto push32 = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)v); };
+            auto push64 = [&](double v) {
+                const uint64_t b = __builtin_bit_cast(uint64_t, v);
+                const uint64_t lo = push32((uint32_t)b), hi = push32((uint32_t)(b >> 32));
+                return __builtin_bit_cast(double, lo | (hi << 32));
+            };
+            x.r.o.x = push64(x.r.o.x), x.r.o.y = push64(x.r.o.y), x.r.o.z = push64(x.r.o.z);
+            x.r.d.x = push64(x.r.d.x), x.r.d.y = push64(x.r.d.y), x.r.d.z = push64(x.r.d.z);
+            if (!(F & F_STATIC)) x.r.t = push64(x.r.t);
+            x.rng = push32(x.rng);
+            x.depth = push32(x.depth);
+            home = push32(home);
+        }
         pf.mark(PS_LOAD);
         if (x.depth != 0) {
             if constexpr (DIRECT) x.r = unpark(tid);
@@ -870,7 +909,7 @@ void k_persist(persist_args) {
                                                         : SS.prims[h.prim].material].type);
 #endif
             // the outcome is applied inside the branch that produced it
-            uint32_t me = tid;
+            uint32_t me = BIN ? home : tid;
             if constexpr (DIRECT) {
                 // the ray again from its slot: the copy the walk used is dead
                 // from here on (a fresh index keeps the compiler from reusing it)
@@ -1157,12 +1196,24 @@ struct fast_args {
     rtwf::cam32 cam;
 };
 
+// fast_args re-read from the kernarg segment by each phase that uses it
+// (args_now's reason: hoisted whole, the scene and job fields fill the
+// SGPRs and spill into VGPR lanes)
+__device__ __forceinline__ const fast_args& fast_args_now() {
+    cptr<fast_args> p = (cptr<fast_args>)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const fast_args*)p;
+}
+
+#ifndef RTW_FAST_BVH_WAVES
+#define RTW_FAST_BVH_WAVES 6
+#endif
 template <int F, bool LST>
-__global__ __launch_bounds__(kBlock) void k_fast(fast_args A) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_FAST_BVH_WAVES)))
+void k_fast(fast_args) {
     using namespace rtwf;
     __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kBlock];
     __shared__ uint32_t s_cnt[kWaves];
-    const fscene& S = A.S;
     const uint32_t lane = threadIdx.x & 63;
     const int own = blockIdx.x % kQShards;
     fray r{f3{0, 0, 0}, f3{0, 0, 1}, 0};
@@ -1174,6 +1225,7 @@ __global__ __launch_bounds__(kBlock) void k_fast(fast_args A) {
         const bool idle = depth == 0;
         const unsigned long long m = __ballot(idle);
         if (open && m) {
+            const fast_args& A = fast_args_now();
             const uint32_t want = (uint32_t)__popcll(m);
             const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
             uint32_t left = want, given = 0, nq = 0;
@@ -1215,98 +1267,25 @@ __global__ __launch_bounds__(kBlock) void k_fast(fast_args A) {
         fhit h;
         if constexpr (LST) {
             lds_stackf stk{&s_stack[0][threadIdx.x]};
-            h = world_closest<F>(S, r, rng, stk);
+            h = world_closest<F>(fast_args_now().S, r, rng, stk);
         } else {
             priv_stackf stk;
-            h = world_closest<F>(S, r, rng, stk);
+            h = world_closest<F>(fast_args_now().S, r, rng, stk);
         }
         ++segs;
         // one segment of color() (RayTracingWeekend.cpp:52-159)
-        bool end = true;
+        const seg_f sg = shade(fast_args_now().S, r, h, rng, depth);
+        bool end = !sg.cont;
         f3 L{0, 0, 0};
-        if (h.prim == -1) {  // background :141-159
-            if (S.background == RTW_BG_GRADIENT) {
-                const float t = 0.5f * (normalize(r.d).y + 1.0f);
-                L = thr * (f3{1, 1, 1} * (1.0f - t) + f3{0.5f, 0.7f, 1.0f} * t);
-            }
+        if (sg.cont) {
+            thr = thr * sg.w;
+            r = sg.next;
+            --depth;
         } else {
-            f3 p, n;
-            int mat, fp;
-            hit_record(S, r, h, p, n, mat, fp);
-            if (S.render_type == RTW_RENDER_NORMAL) {  // :135-136
-                L = thr * ((n + f3{1, 1, 1}) * 0.5f);
-            } else {
-                const mat32& M = S.materials[mat];
-                const int type = M.type;
-                if (type == RTW_MAT_DIFFUSE_LIGHT) {  // material.h:232-244, one-sided
-                    if (dot(n, r.d) > 0) L = thr * texture_value(S, M.texture, p);
-                } else {
-                    f3 f{1, 1, 1}, dir;
-                    bool alive = true;
-                    if (type == RTW_MAT_METAL) {  // material.h:128-136
-                        dir = reflect(normalize(r.d), n) + rtwf::random_in_unit_sphere(rng) * M.fuzz;
-                        f = ldf3(M.albedo);
-                    } else if (type == RTW_MAT_DIELECTRIC) {  // material.h:146-222
-                        const float dn = dot(r.d, n), il = __builtin_amdgcn_rsqf(len2(r.d));
-                        const float ri = M.ref_idx;
-                        f3 outward;
-                        float ni, cosine;
-                        if (dn > 0) {
-                            outward = -n;
-                            ni = ri;
-                            cosine = dn * il;
-                            cosine = fsqrt(__builtin_fmaxf(0.0f, 1 - ri * ri * (1 - cosine * cosine)));
-                        } else {
-                            outward = n;
-                            ni = M.inv_ref_idx;
-                            cosine = -dn * il;
-                        }
-                        const f3 uv = r.d * il;
-                        const float dt = dot(uv, outward);
-                        const float disc = 1.0f - ni * ni * (1 - dt * dt);
-                        f3 refracted{0, 0, 0};
-                        float reflect_prob = 1.0f;
-                        if (disc > 0) {
-                            refracted = (uv - outward * dt) * ni - outward * fsqrt(disc);
-                            const float x = 1 - cosine, x2 = x * x;
-                            reflect_prob = M.r0 + (1 - M.r0) * (x2 * x2 * x);
-                        }
-                        dir = u01(rng) < reflect_prob ? reflect(r.d, n) : refracted;
-                    } else if (type == RTW_MAT_ISOTROPIC) {  // material.h:257-262
-                        dir = rtwf::random_in_unit_sphere(rng);
-                        f = texture_value(S, M.texture, p);
-                    } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
-                        const onbf fr = frame(S, n, fp);
-                        float pdf_val;
-                        if (S.n_lights > 0) {
-                            dir = mixture_generate(S, fr, p, rng);
-                            const float cw = dot(normalize(dir), fr.w);
-                            pdf_val = 0.5f * (cw <= 0 ? 0.0f : cw * (1.0f / kPiF)) + 0.5f * lights_pdf_value(S, p, dir);
-                        } else {
-                            const float r1 = u01(rng), r2 = u01(rng);
-                            dir = local(fr, cone_dir(r1, fsqrt(1 - r2)));
-                            const float cw = dot(normalize(dir), fr.w);
-                            pdf_val = cw <= 0 ? 0.0f : cw * (1.0f / kPiF);
-                        }
-                        if (pdf_val > 0) {
-                            const float cosine = dot(n, normalize(dir));
-                            const float spdf = cosine < 0 ? 0.0f : cosine * (1.0f / kPiF);
-                            f = texture_value(S, M.texture, p) * (spdf * rcp(pdf_val));
-                        } else {
-                            alive = false;  // :126-127 returns emitted (0)
-                        }
-                    }
-                    if (alive && depth > 1) {  // the next color() call has depth - 1
-                        thr = thr * f;
-                        r = fray{p, dir, r.t};
-                        --depth;
-                        end = false;
-                    }
-                }
-            }
+            L = thr * sg.w;
         }
         if (end) {
-            double* o = A.J.L + 3 * (size_t)q;
+            double* o = fast_args_now().J.L + 3 * (size_t)q;
             o[0] = (double)L.x, o[1] = (double)L.y, o[2] = (double)L.z;
             depth = 0;
         }
@@ -1317,7 +1296,189 @@ __global__ __launch_bounds__(kBlock) void k_fast(fast_args A) {
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
         for (int k = 0; k < kWaves; ++k) t += s_cnt[k];
-        if (t) atomicAdd(&A.C->segments[blockIdx.x % 8].v, t);
+        if (t) atomicAdd(&fast_args_now().C->segments[blockIdx.x % 8].v, t);
+    }
+}
+
+// Re-point an fp32 scene's arrays into an LDS copy of its allocation.
+__device__ __forceinline__ rtwf::fscene lds_fscene(const rtwf::fscene& S, const char* base, uint32_t bytes,
+                                                   const char* lds) {
+    rtwf::fscene L = S;
+    auto rb = [&](const void* p) -> const void* {
+        const char* c = (const char*)p;
+        return (c && c >= base && c < base + bytes) ? (const void*)(lds + (c - base)) : p;
+    };
+    L.prims = (const rtwf::prim32*)rb(S.prims);
+    L.entries = (const rtwf::ent32*)rb(S.entries);
+    L.ops = (const rtwf::op32*)rb(S.ops);
+    L.materials = (const rtwf::mat32*)rb(S.materials);
+    L.textures = (const rtwf::tex32*)rb(S.textures);
+    L.lights = (const rtw_light*)rb(S.lights);
+    L.ranvec = (const float*)rb(S.ranvec);
+    L.perm = (const int32_t*)rb(S.perm);
+    L.frames = (const float*)rb(S.frames);
+    return L;
+}
+
+// fp32 fast mode with material regrouping (list scenes, as k_persist_sort
+// for fp64): after each traversal the block's 256 paths are counting-sorted
+// by what their hit needs and moved through LDS to the lane of their rank,
+// so most waves run one shading branch; idle lanes gather at the top and take
+// camera samples there.  Paths wait between iterations in their lane's LDS
+// slot; throughputs stay in home slots.  LDS: the fp32 scene (when it fits)
+// for shading, traversal reads the scene through the scalar cache.
+#ifndef RTW_FAST_WAVES
+#define RTW_FAST_WAVES 6  // T fp32: 6 465 (5 waves), 5 601 (4), 7 000 (6)
+#endif
+template <int F, bool LDS>
+__global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(RTW_FAST_WAVES)))
+void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
+    using namespace rtwf;
+    extern __shared__ __attribute__((aligned(16))) char s_scene[];
+    __shared__ uint32_t s_kc[kSortWaves][FK_N];
+    __shared__ uint32_t s_seg[kSortWaves];
+    __shared__ float x_o[3][kSortBlock], x_d[3][kSortBlock], x_tm[kSortBlock], x_t[kSortBlock];
+    __shared__ int32_t x_prim[kSortBlock];
+    __shared__ uint32_t x_rng[kSortBlock], x_depth[kSortBlock], x_q[kSortBlock], x_home[kSortBlock];
+    __shared__ float s_thr[3][kSortBlock];
+    x_home[threadIdx.x] = threadIdx.x;
+    if (LDS) {
+        const uint4* src = reinterpret_cast<const uint4*>(base);
+        uint4* dst = reinterpret_cast<uint4*>(s_scene);
+        for (uint32_t k = threadIdx.x; k < bytes / 16; k += kSortBlock) dst[k] = src[k];
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int own = blockIdx.x % kQShards;
+    uint32_t rng = 0, depth = 0, segs = 0;
+    bool open = true;  // wave-uniform: the queue may still hold samples
+    for (;;) {
+        const uint32_t me = threadIdx.x;
+        // 1. idle lanes take new camera samples (one reservation per wave)
+        {
+            const bool idle = depth == 0;
+            const unsigned long long m = __ballot(idle);
+            if (open && m) {
+                const fast_args& A = fast_args_now();
+                const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+                uint32_t left = (uint32_t)__popcll(m), given = 0, q = 0;
+                bool got = false;
+                for (int a = 0; a < kQShards && left; ++a) {
+                    const int sh = (own + a) % kQShards;
+                    const unsigned long long lim = shard_limit(sh, A.J.total);
+                    unsigned long long b = ~0ull;
+                    if (lane == 0) {
+                        const bool dry = a > 0 && __hip_atomic_load(&A.C->qshard[sh].v, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT) >= lim;
+                        if (!dry) b = atomicAdd(&A.C->qshard[sh].v, (unsigned long long)left);
+                    }
+                    b = __shfl(b, 0, 64);
+                    if (b == ~0ull || b >= lim) continue;
+                    const uint32_t ok = (uint32_t)min((unsigned long long)left, lim - b);
+                    if (idle && rank >= given && rank < given + ok) {
+                        q = (uint32_t)shard_sample(sh, b + (rank - given));
+                        got = true;
+                    }
+                    given += ok;
+                    left -= ok;
+                }
+                if (left) open = false;
+                if (got) {
+                    int i, j, sm;
+                    sample_coords(A.J, q, i, j, sm);
+                    rng = path_seed(A.J.seed_mix, (uint32_t)(j * A.J.nx + i), (uint32_t)sm);
+                    const float u = ((float)i + u01(rng)) * rcp((float)A.J.nx);
+                    const float v = ((float)j + u01(rng)) * rcp((float)A.J.ny);
+                    const fray r = camera_ray(A.cam, u, v, rng);
+                    x_o[0][me] = r.o.x, x_o[1][me] = r.o.y, x_o[2][me] = r.o.z;
+                    x_d[0][me] = r.d.x, x_d[1][me] = r.d.y, x_d[2][me] = r.d.z;
+                    x_tm[me] = r.t;
+                    x_q[me] = q;
+                    depth = (uint32_t)A.J.max_depth;
+                    const uint32_t home = x_home[me];
+                    s_thr[0][home] = 1.0f, s_thr[1][home] = 1.0f, s_thr[2][home] = 1.0f;
+                }
+            }
+        }
+        // 2. traversal
+        fhit h{0.0f, -1, false};
+        int key = FK_IDLE;
+        fray r;
+        if (depth != 0) {
+            r = fray{f3{x_o[0][me], x_o[1][me], x_o[2][me]}, f3{x_d[0][me], x_d[1][me], x_d[2][me]}, x_tm[me]};
+            priv_stackf stk;
+            h = world_closest<F>(fast_args_now().S, r, rng, stk);
+            ++segs;
+            const fast_args& A = fast_args_now();
+            key = hit_key(LDS ? lds_fscene(A.S, base, bytes, s_scene) : A.S, h);
+        }
+        // 3. counting sort of the block's paths by key
+        const uint32_t my_home = x_home[me], my_q = x_q[me];
+        uint32_t rank_in_wave = 0;
+#pragma unroll
+        for (int k = 0; k < FK_N; ++k) {
+            const unsigned long long m = __ballot(key == k);
+            if (key == k) rank_in_wave = (uint32_t)__popcll(m & lanemask_lt());
+            if (lane == 0) s_kc[wave][k] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        uint32_t dst = rank_in_wave, idle_total = 0;
+#pragma unroll
+        for (int k = 0; k < FK_N; ++k) {
+            uint32_t tot = 0, before = 0;
+#pragma unroll
+            for (int w = 0; w < kSortWaves; ++w) {
+                const uint32_t c = s_kc[w][k];
+                tot += c;
+                before += (w < (int)wave) ? c : 0u;
+            }
+            if (k < key) dst += tot;
+            if (k == key) dst += before;
+            if (k == FK_IDLE) idle_total = tot;
+        }
+        if (idle_total == kSortBlock) break;  // block-uniform: nothing left to trace or take
+        // 4. move every path to the slot of its rank
+        if (depth != 0) {
+            x_o[0][dst] = r.o.x, x_o[1][dst] = r.o.y, x_o[2][dst] = r.o.z;
+            x_d[0][dst] = r.d.x, x_d[1][dst] = r.d.y, x_d[2][dst] = r.d.z;
+            x_tm[dst] = r.t;
+        }
+        x_home[dst] = my_home;
+        x_t[dst] = h.t;
+        x_prim[dst] = h.prim;
+        x_rng[dst] = rng;
+        x_depth[dst] = depth;
+        x_q[dst] = my_q;
+        __syncthreads();
+        rng = x_rng[me];
+        depth = x_depth[me];
+        // 5. shading, now mostly one branch per wave
+        if (depth != 0) {
+            const fray rr{f3{x_o[0][me], x_o[1][me], x_o[2][me]}, f3{x_d[0][me], x_d[1][me], x_d[2][me]}, x_tm[me]};
+            const fhit hh{x_t[me], x_prim[me], false};
+            const fast_args& A = fast_args_now();
+            const seg_f sg = shade(LDS ? lds_fscene(A.S, base, bytes, s_scene) : A.S, rr, hh, rng, depth);
+            const uint32_t home = x_home[me];
+            const f3 thr{s_thr[0][home], s_thr[1][home], s_thr[2][home]};
+            if (sg.cont) {
+                s_thr[0][home] = thr.x * sg.w.x, s_thr[1][home] = thr.y * sg.w.y, s_thr[2][home] = thr.z * sg.w.z;
+                x_o[0][me] = sg.next.o.x, x_o[1][me] = sg.next.o.y, x_o[2][me] = sg.next.o.z;
+                x_d[0][me] = sg.next.d.x, x_d[1][me] = sg.next.d.y, x_d[2][me] = sg.next.d.z;
+                --depth;
+            } else {
+                double* o = A.J.L + 3 * (size_t)x_q[me];
+                o[0] = (double)(thr.x * sg.w.x), o[1] = (double)(thr.y * sg.w.y), o[2] = (double)(thr.z * sg.w.z);
+                depth = 0;
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_down(segs, off, 64);
+    if (lane == 0) s_seg[wave] = segs;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int k = 0; k < kSortWaves; ++k) t += s_seg[k];
+        if (t) atomicAdd(&fast_args_now().C->segments[blockIdx.x % 8].v, t);
     }
 }
 
@@ -1593,6 +1754,7 @@ struct handle_t {
     dev_buf scene_mem;
     dev_buf scene32;  // fp32 mirror of the scene (fast mode, rtw_fast.h)
     rtwf::fscene F32{};
+    uint32_t f32_bytes = 0;  // bytes of scene32 fp32 shading reads
     dev_buf pool[2];  // path SoA, ping-pong for compaction
     dev_buf fresh;    // staging of new camera rays (fresh_t)
     dev_buf hits;
@@ -2118,15 +2280,21 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             o.type = T.type, o.odd = T.odd, o.even = T.even, o.scale = (float)T.scale;
             for (int j = 0; j < 3; ++j) o.color[j] = (float)T.color[j];
         }
-        std::vector<float> rv32(768, 0.0f), fr32(frames.size());
-        if (d->has_perlin)
-            for (int k = 0; k < 768; ++k) rv32[k] = (float)d->perlin_ranvec[k];
+        std::vector<float> rv32(d->has_perlin ? 768 : 0), fr32(frames.size());
+        for (size_t k = 0; k < rv32.size(); ++k) rv32[k] = (float)d->perlin_ranvec[k];
         for (size_t k = 0; k < frames.size(); ++k) fr32[k] = (float)frames[k];
+        // everything fp32 shading reads, in one allocation: the prefix the
+        // regrouping kernel stages in LDS (k_fast_sort)
         std::vector<part> p2 = {
-            {p32.data(), sizeof(prim32) * p32.size(), 0},   {e32.data(), sizeof(ent32) * e32.size(), 0},
-            {o32.data(), sizeof(op32) * o32.size(), 0},     {m32.data(), sizeof(mat32) * m32.size(), 0},
-            {t32.data(), sizeof(tex32) * t32.size(), 0},    {rv32.data(), sizeof(float) * rv32.size(), 0},
+            {p32.data(), sizeof(prim32) * p32.size(), 0},
+            {e32.data(), sizeof(ent32) * e32.size(), 0},
+            {o32.data(), sizeof(op32) * o32.size(), 0},
+            {m32.data(), sizeof(mat32) * m32.size(), 0},
+            {t32.data(), sizeof(tex32) * t32.size(), 0},
+            {rv32.data(), sizeof(float) * rv32.size(), 0},
             {fr32.data(), sizeof(float) * fr32.size(), 0},
+            {d->lights, sizeof(rtw_light) * d->n_lights, 0},
+            {d->has_perlin ? d->perlin_perm : nullptr, d->has_perlin ? sizeof(int32_t) * 768 : 0, 0},
         };
         size_t tot = 0;
         for (auto& x : p2) {
@@ -2136,7 +2304,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         if ((rc = h->scene32.ensure(std::max<size_t>(tot, 256)))) return rc;
         std::vector<char> st2(std::max<size_t>(tot, 256), 0);
         for (auto& x : p2)
-            if (x.bytes) std::memcpy(st2.data() + x.off, x.src, x.bytes);
+            if (x.bytes && x.src) std::memcpy(st2.data() + x.off, x.src, x.bytes);
         HIPCHK(hipMemcpy(h->scene32.p, st2.data(), st2.size(), hipMemcpyHostToDevice));
         char* b2 = static_cast<char*>(h->scene32.p);
         fscene& F = h->F32;
@@ -2145,14 +2313,18 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         F.ops = (const op32*)(b2 + p2[2].off);
         F.materials = (const mat32*)(b2 + p2[3].off);
         F.textures = (const tex32*)(b2 + p2[4].off);
-        F.ranvec = (const float*)(b2 + p2[5].off);
+        F.ranvec = p2[5].bytes ? (const float*)(b2 + p2[5].off) : nullptr;
         F.frames = (const float*)(b2 + p2[6].off);
-        F.lights = S.lights;
-        F.perm = S.perm;
+        F.lights = p2[7].bytes ? (const rtw_light*)(b2 + p2[7].off) : nullptr;
+        F.perm = p2[8].bytes ? (const int32_t*)(b2 + p2[8].off) : nullptr;
+        h->f32_bytes = (uint32_t)(p2[8].off + p2[8].bytes);
         F.nodes = S.nodes;
         F.items = S.items;
         F.runs = S.runs;
         F.media = S.media;
+        F.ysph = S.ysph;
+        F.mv_t0 = (float)S.mv_t0;
+        F.mv_inv_den = (float)(1.0 / S.mv_den);
         F.light_weight = (float)S.light_weight;
         F.n_lights = S.n_lights;
         F.world_bvh_root = S.world_bvh_root;
@@ -2388,8 +2560,36 @@ void launch_fast_t(bool probe, std::string* name, int cus, hipStream_t st, const
     const int grid = blocks_per_cu(reinterpret_cast<const void*>(&k_fast<FF, LST>), kBlock, 0) * cus;
     hipLaunchKernelGGL((k_fast<FF, LST>), dim3(grid), dim3(kBlock), 0, st, A);
 }
+template <int FF, bool LL>
+void launch_fast_sort_t(bool probe, std::string* name, int cus, hipStream_t st, const fast_args& A,
+                        const char* base, uint32_t bytes) {
+    if (name) *name = kname("k_fast_sort", FF, -1, LL ? 1 : 0);
+    if (probe) return;
+    const size_t shm = LL ? bytes : 0;
+    const int grid = blocks_per_cu(reinterpret_cast<const void*>(&k_fast_sort<FF, LL>), kSortBlock, shm) * cus;
+    hipLaunchKernelGGL((k_fast_sort<FF, LL>), dim3(grid), dim3(kSortBlock), shm, st, A, base, bytes);
+}
+// RTW_FAST_SORT=0: list scenes take k_fast too (A/B)
+bool fast_sort_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("RTW_FAST_SORT");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    return on;
+}
 void launch_fast(bool probe, const handle_t* h, hipStream_t st, const fast_args& A, std::string* name = nullptr) {
     const int f = h->features & (F_MEDIA | F_WBVH | F_GBVH);
+    if ((f & (F_WBVH | F_GBVH)) == 0 && fast_sort_enabled()) {  // list scenes: regrouping kernel
+        const char* base = static_cast<const char*>(h->scene32.p);
+        const bool lds = h->f32_bytes <= kShadeLdsMax;
+        if (f == F_MEDIA)
+            lds ? launch_fast_sort_t<F_MEDIA, true>(probe, name, h->cus, st, A, base, h->f32_bytes)
+                : launch_fast_sort_t<F_MEDIA, false>(probe, name, h->cus, st, A, base, h->f32_bytes);
+        else
+            lds ? launch_fast_sort_t<0, true>(probe, name, h->cus, st, A, base, h->f32_bytes)
+                : launch_fast_sort_t<0, false>(probe, name, h->cus, st, A, base, h->f32_bytes);
+        return;
+    }
     const bool lst = (f & (F_WBVH | F_GBVH)) && h->stack_need <= kLdsStack && h->S.n_nodes < 65536;
     switch (f * 2 + (lst ? 1 : 0)) {
 #define RTW_FAST(FF, LL) \

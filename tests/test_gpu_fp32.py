@@ -67,7 +67,7 @@ def test_fast_mode_is_statistically_the_reference(gpu, scene, nx, ny, spp, depth
     for acc, st in fast:
         assert st["samples"] == nx * ny * spp and np.all(np.isfinite(acc))
         assert st["bytes_intersect"] == 36 * st["segments"]
-    assert info["kernel_fast"].startswith("k_fast<")
+    assert info["kernel_fast"].startswith(("k_fast<", "k_fast_sort<"))
     rb = blocks(ref, nx, ny, spp)
     d = np.concatenate([blocks(acc, nx, ny, spp) - rb for acc, _ in fast])
     e = np.concatenate([blocks(acc, nx, ny, spp) - rb for acc, _ in other])
