@@ -38,8 +38,9 @@ kernel, build = roofs[0]["kernel"], roofs[0]["build_id"]
 cfg = lines[0]["config"]
 
 
-class _A:  # pmc_key(args) wants scene / nx / ny / depth / bvh
+class _A:  # pmc_key(args) wants scene / nx / ny / depth / bvh / precision
     scene, nx, ny, depth, bvh = cfg["scene"], cfg["nx"], cfg["ny"], cfg["max_depth"], cfg["bvh"]
+    precision = cfg.get("precision", "fp64")
 
 
 key = pmc_key(_A)

@@ -21,5 +21,7 @@ scripts/prof_kernels.sh T_$tag --steps 3 --warmup 1 --no-cpu-baseline
 bash scripts/pmc_workloads.sh $tag > gpurun_out/pmc_$tag.txt 2>&1
 cp gpurun_out/pmc/*_$tag.json profiles/pmc/
 timeout -k 10 300 python bench.py > gpurun_out/bench_T_$tag.txt 2>&1
-bash scripts/bench_configs.sh $tag > /dev/null
 tail -1 gpurun_out/bench_T_$tag.txt | cut -c1-200
+bash scripts/bench_configs.sh $tag > /dev/null
+bash scripts/bench_fp32.sh $tag > /dev/null
+bash scripts/full_configs.sh $tag > /dev/null
