@@ -24,6 +24,21 @@ namespace rtwd {
 
 constexpr double kPi = 3.14159265358979323846;
 constexpr double kTwoPi = 2 * kPi;                 // `2 * M_PI` (exact doubling)
+constexpr double kInvPi = 1.0 / kPi;
+
+// RTW_RADIANCE_FAST: a path's radiance is the product of per-bounce factors
+// (attenuation * scattering_pdf / pdf) and the emission it ends on; those
+// values never steer a path -- no branch, ray or random draw of the
+// reference reads them, only the SIGN of pdf_val (RayTracingWeekend.cpp:
+// 126-127) -- so they may be formed with fewer divisions: the lambertian
+// factor as texture * (cosine / (pi pdf_val)) (one division instead of
+// four), cosine / pi as cosine * (1 / pi) (the same sign: both round the same
+// positive real), the rect light's distance^2 / (cosine area) with one
+// division.  Paths, traversal counts and every decision stay the
+// reference's; the radiance moves by a few ulps (the parity bound is 1e-4).
+#ifndef RTW_RADIANCE_FAST
+#define RTW_RADIANCE_FAST 1
+#endif
 constexpr double kDblMax = 1.7976931348623157e308; // std::numeric_limits<double>::max()
 constexpr double kFltMax = 3.4028234663852886e38;  // FLT_MAX widened
 constexpr double kTMin = (double)0.001f;           // RayTracingWeekend.cpp:52 (float literal)
@@ -1382,8 +1397,13 @@ RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
         if (!rect_t(q, r, 0.001, __builtin_inf(), t)) return 0;
         const double area = (q.p[1] - q.p[0]) * (q.p[3] - q.p[2]);
         const double distance_squared = t * t * len2(v);
+#if RTW_RADIANCE_FAST
+        // |dot(v, n)| / |v| folded into one quotient (v.y != 0: the rect was hit)
+        return distance_squared * len(v) / (fabs(v.y) * area);
+#else
         const double cosine = fabs(dot(v, d3{0, 1, 0}) / len(v));
         return distance_squared / (cosine * area);
+#endif
     }
     if (L.kind == RTW_LIGHT_SPHERE) {  // sphere.h:88-99
         const rtw_prim& q = S.prims[L.prim];

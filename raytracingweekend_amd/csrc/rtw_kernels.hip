@@ -451,6 +451,11 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
         const d3 dir = random_in_unit_sphere(rng);
         return scatter(texture_value<M>(S, m.texture, p), p, dir);
     } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
+        // (RTW_RADIANCE_FAST: quantities that only scale radiance -- the
+        // attenuation / pdf factor and the pdfs' magnitudes -- are formed with
+        // fewer divisions than the reference's expressions; everything a
+        // decision reads -- directions, t, the sign of pdf_val -- is the
+        // reference's own arithmetic.  See RTW_RADIANCE_FAST below.)
         // onb::build_from_w(normal) (onb.h:32-38), built where it is used
         const surf_frame sf{n, prim, rect};
         pf.mark(PS_HIT);
@@ -465,24 +470,30 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
             const d3 ud = normalize(dir);
             const double cw = dot(ud, frame_w(S, sf));
             cosine = dot(n, ud);  // material.h:115-119
-            const double p0 = (cw <= 0) ? 0 : cw / kPi;
+            const double p0 = (cw <= 0) ? 0 : (RTW_RADIANCE_FAST ? cw * kInvPi : cw / kPi);
             pdf_val = 0.5 * p0 + 0.5 * lights_pdf_value<STATIC>(S, p, dir);
         } else {
             dir = local(frame_onb(S, sf), random_cosine_direction(rng));
             const d3 ud = normalize(dir);
             const double cw = dot(ud, frame_w(S, sf));
             cosine = dot(n, ud);  // material.h:115-119
-            pdf_val = (cw <= 0) ? 0 : cw / kPi;
+            pdf_val = (cw <= 0) ? 0 : (RTW_RADIANCE_FAST ? cw * kInvPi : cw / kPi);
         }
         if (pdf_val <= 0.0) {  // :126-127 returns emitted (= 0)
             sk.end_zero();
             return SEG_END_ZERO;
         }
-        const double spdf = cosine < 0 ? 0 : cosine / kPi;
         pf.mark(PS_PDF);
         // attenuation = texture value (material.h:98), read only now: it
         // draws nothing, and a late read keeps it out of the busiest registers
+#if RTW_RADIANCE_FAST
+        // attenuation * scattering_pdf / pdf_val as one scalar quotient
+        const double w = cosine < 0 ? 0 : cosine / (kPi * pdf_val);
+        return scatter(texture_value<M>(S, m.texture, p) * w, p, dir);
+#else
+        const double spdf = cosine < 0 ? 0 : cosine / kPi;
         return scatter((texture_value<M>(S, m.texture, p) * spdf) / pdf_val, p, dir);
+#endif
     }
 }
 
