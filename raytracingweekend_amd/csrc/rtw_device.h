@@ -821,28 +821,68 @@ RTW_D void arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_sta
     }
 }
 
+// arbitrate with a wave-uniform prim index (packet walks): the prim's fields
+// are scalar loads, and the walk's shared 1 / dot(d, d) serves the sphere
+// roots (walk_quot's rules; t_min = 0.001)
+RTW_D void arbitrate_u(const scene& S, int pi, const ray& r, double t_min, hit_state& h, double fc, double ya,
+                       bool oka) {
+    const rtw_prim q = uprim(S.prims, pi);
+    const bool rl = !is_sphere(q.type);
+    double t;
+    if (rl) {
+        if (!rect_t(q, r, t_min, h.t, t)) return;
+    } else {
+        const d3 oc = r.o - sphere_center(q, r.t, fc);
+        const double a = dot(r.d, r.d);
+        const double b = dot(oc, r.d);
+        const double c = dot(oc, oc) - q.p[9];
+        const double disc = b * b - a * c;
+        if (!(disc > 0)) return;
+        const double sq = __builtin_sqrt(disc);
+        t = walk_quot(-b - sq, a, ya, oka);
+        if (!(t < kDblMax && t > t_min)) {
+            t = walk_quot(-b + sq, a, ya, oka);
+            if (!(t < kDblMax && t > t_min)) return;
+        }
+        if (t > h.t) return;
+    }
+    if (better(t, pi, rl, h.t, h.prim, h.rect, h.prim != -1)) {
+        h.t = t;
+        h.prim = pi;
+        h.rect = rl;
+    }
+}
+
 // A box item of a group BVH (RTW_ITEM_BOX): its six rects in the box's list
 // order (hittable_list.h:65-114: +z, -z, +y, -y, +x, -x), each with the
 // reference's own test and better()'s tie rule -- exactly six arbitrate
 // calls, with each rect's plane axis known instead of read from its type.
-template <int K, int A, int B>
+// (U: the box index is wave-uniform, a packet walk's: the rects' fields are
+// scalar loads)
+template <int K, int A, int B, bool U = false>
 RTW_D void rect_arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_state& h) {
-    const rtw_prim& q = S.prims[pi];  // fields read where the test uses them
     double t;
-    if (!rect_axis_t<K, A, B>(q, r, t_min, h.t, t)) return;
+    if constexpr (U) {
+        const rtw_prim q = uprim(S.prims, pi);
+        if (!rect_axis_t<K, A, B>(q, r, t_min, h.t, t)) return;
+    } else {
+        const rtw_prim& q = S.prims[pi];  // fields read where the test uses them
+        if (!rect_axis_t<K, A, B>(q, r, t_min, h.t, t)) return;
+    }
     if (better(t, pi, true, h.t, h.prim, h.rect, h.prim != -1)) {
         h.t = t;
         h.prim = pi;
         h.rect = true;
     }
 }
+template <bool U = false>
 RTW_D void box_arbitrate(const scene& S, int first, const ray& r, double t_min, hit_state& h) {
-    rect_arbitrate<2, 0, 1>(S, first, r, t_min, h);
-    rect_arbitrate<2, 0, 1>(S, first + 1, r, t_min, h);
-    rect_arbitrate<1, 0, 2>(S, first + 2, r, t_min, h);
-    rect_arbitrate<1, 0, 2>(S, first + 3, r, t_min, h);
-    rect_arbitrate<0, 1, 2>(S, first + 4, r, t_min, h);
-    rect_arbitrate<0, 1, 2>(S, first + 5, r, t_min, h);
+    rect_arbitrate<2, 0, 1, U>(S, first, r, t_min, h);
+    rect_arbitrate<2, 0, 1, U>(S, first + 1, r, t_min, h);
+    rect_arbitrate<1, 0, 2, U>(S, first + 2, r, t_min, h);
+    rect_arbitrate<1, 0, 2, U>(S, first + 3, r, t_min, h);
+    rect_arbitrate<0, 1, 2, U>(S, first + 4, r, t_min, h);
+    rect_arbitrate<0, 1, 2, U>(S, first + 5, r, t_min, h);
 }
 // a group-BVH leaf item: a prim, or a box's six rects
 RTW_D void arbitrate_item(const scene& S, int it, const ray& r, double t_min, hit_state& h, double fc) {
@@ -850,6 +890,14 @@ RTW_D void arbitrate_item(const scene& S, int it, const ray& r, double t_min, hi
         box_arbitrate(S, it & RTW_ITEM_INDEX, r, t_min, h);
     else
         arbitrate(S, it, r, t_min, h, fc);
+}
+// ... with a wave-uniform item (packet walks); arbitrate_u without a shared
+// reciprocal divides exactly, as arbitrate does
+RTW_D void arbitrate_item_u(const scene& S, int it, const ray& r, double t_min, hit_state& h, double fc) {
+    if (it & RTW_ITEM_BOX)
+        box_arbitrate<true>(S, it & RTW_ITEM_INDEX, r, t_min, h);
+    else
+        arbitrate_u(S, it, r, t_min, h, fc, 0.0, false);
 }
 
 // arbitrate for a world walk's one-prim leaves with the walk's shared
@@ -896,11 +944,15 @@ RTW_HD int node_count(const bvh_node32& n) { return n.b < 0 ? -n.b : 0; }
 
 // Per-walk fp32 form of the ray for the slab tests: t = x * inv + oi per
 // axis, with oi = -o * inv moved down (oin, near planes) and up (oif, far
-// planes) by eps = 2^-21 (B + |o|) |inv|, B the largest node coordinate
-// (scene::bvh_bound).  eps covers the fp32 rounding of inv (x * inv is off by
-// at most 2^-23.9 B |inv|) and of oi itself, so x * inv + oin <= (x - o) / d
-// <= x * inv + oif in real arithmetic.  An axis whose |inv| or eps exceeds
-// 2^90 (d.K ~ 0, NaN) never culls: inv = 0, oin = -inf, oif = +inf.
+// planes) by eps = (2^-21 + 2^-22) (B + |o|) |inv| + 2^-120, B the largest
+// node coordinate (scene::bvh_bound).  The 2^-21 part covers the fp32
+// rounding of inv (x * inv is off by at most 2^-23.9 B |inv|) and of oi
+// itself, so x * inv + oin <= (x - o) / d <= x * inv + oif in real
+// arithmetic; the 2^-22 part covers the rounding of the slab test's own fma
+// (its result is at most (B + |o|) |inv| (1 + 2^-20) in magnitude, so it is
+// off by less than 2^-23.9 of that), and 2^-120 a flushed denormal result.
+// An axis whose |inv| or eps exceeds 2^90 (d.K ~ 0, NaN) never culls:
+// inv = 0, oin = -inf, oif = +inf.
 struct slab_ray {
     float inv[3], oin[3], oif[3];
 };
@@ -911,7 +963,7 @@ RTW_D slab_ray make_slab_ray(const scene& S, const ray& r) {
     for (int k = 0; k < 3; ++k) {
         const double inv = 1.0 / dd[k];
         const double oi = -oo[k] * inv;
-        const double eps = 0x1p-21 * (S.bvh_bound + __builtin_fabs(oo[k])) * __builtin_fabs(inv);
+        const double eps = 0x1.8p-21 * (S.bvh_bound + __builtin_fabs(oo[k])) * __builtin_fabs(inv) + 0x1p-120;
         const bool ok = __builtin_fabs(inv) <= 0x1p90 && eps <= 0x1p90;
         s.inv[k] = ok ? (float)inv : 0.0f;
         s.oin[k] = ok ? (float)(oi - eps) : -__builtin_inff();
@@ -920,15 +972,14 @@ RTW_D slab_ray make_slab_ray(const scene& S, const ray& r) {
     return s;
 }
 
-// Slab test of a node over [t0, t1] (already widened by the caller): true
-// whenever the real-arithmetic slab test against the builder's padded fp64
-// bounds is (the fp64 test this replaces was itself conservative that way),
-// so it may keep a node that test would drop, never the reverse.  Per axis
-// the near / far planes' t are bracketed by oin / oif (make_slab_ray); the
-// fp32 rounding of each fma and of t0 / t1 (<= 2^-24 relative) is absorbed
-// by moving the final tn down and tf up by 2^-22 relative + 2^-100 absolute
-// (covers denormal flushing).  Node coordinates are finite and within 2^90
-// (upload), so no NaN arises.
+// Slab test of a node over [t0, t1]: true whenever the real-arithmetic slab
+// test against the builder's padded fp64 bounds is (the fp64 test this
+// replaces was itself conservative that way), so it may keep a node that test
+// would drop, never the reverse.  Per axis the near / far planes' t are
+// bracketed by the fma results (make_slab_ray's eps covers their rounding),
+// min / max are exact, and t0 <= t_min, t1 >= t_max are the caller's (t_lo32,
+// t_hi32): no adjustment is left for the comparison.  Node coordinates are
+// finite and within 2^90 (upload), so no NaN arises.
 RTW_D bool slab32(const bvh_node32& nd, const slab_ray& s, float t0, float t1) {
     float tn = t0, tf = t1;
 #pragma unroll
@@ -940,9 +991,7 @@ RTW_D bool slab32(const bvh_node32& nd, const slab_ray& s, float t0, float t1) {
         tn = __builtin_fmaxf(tn, __builtin_fminf(an, bn));
         tf = __builtin_fminf(tf, __builtin_fmaxf(af, bf));
     }
-    const float tn_adj = __builtin_fmaf(__builtin_fabsf(tn), -0x1p-22f, tn) - 0x1p-100f;
-    const float tf_adj = __builtin_fmaf(__builtin_fabsf(tf), 0x1p-22f, tf) + 0x1p-100f;
-    return tn_adj <= tf_adj;
+    return tn <= tf;
 }
 
 // BVH traversal stacks.  A private array (scratch memory) by default; the
@@ -961,6 +1010,11 @@ struct lds_stack {  // 16-bit node indices (LDS stacks need < 65536 nodes: uploa
     static constexpr int cap = kLdsStack;
     uint16_t* p;  // &column[0][lane]; entry i at p[i * 256]
     RTW_D uint16_t& at(int i) { return p[i * 256]; }
+    // a packet walk's wave-uniform stack: row 0 of the wave's 64 columns
+    static constexpr int wave_cap = 64;
+    RTW_D uint16_t* wave_row() const {
+        return p - __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    }
 };
 
 // A BVH node: from the LDS packet when it is one of the top n_lnodes, else
@@ -987,6 +1041,18 @@ RTW_D bvh_node32 node_at(const scene& S, int i) {
     return nd;
 }
 
+// A node at a wave-uniform index (packet walks): scalar loads through the
+// scalar cache, the fields land in SGPRs.
+RTW_D bvh_node32 node_s(const scene& S, int i) {
+    bvh_node32 nd;
+    const bvh_node32* p = S.nodes + i;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) nd.lo[k] = ld(&p->lo[k]), nd.hi[k] = ld(&p->hi[k]);
+    nd.a = ld(&p->a);
+    nd.b = ld(&p->b);
+    return nd;
+}
+
 // Inner nodes carry their children's split axis (pad & 3) and whether the
 // left child lies on the upper side of it (pad & 4), set at upload: the
 // child nearer along the ray is pushed last, so it is visited first and the
@@ -1009,6 +1075,16 @@ RTW_D void push_children(const bvh_node32& nd, int dneg, STK& stk, int& sp) {
 
 RTW_D double widen_lo(double t) { return t > 0 ? t * 0.5 : t * 2.0 - 1e-9; }
 RTW_D double widen_hi(double t) { return t * (1 + 1e-12) + 1e-9; }
+// fp32 bounds of a walk's t range for slab32: t_lo32(t) <= t (widen_lo leaves
+// a factor of two, the conversion is off by 2^-24 relative); t_hi32(t) >= t
+// (the conversion of widen_hi(t) may round down by 2^-24 relative, so the
+// result is moved up by 2^-23 relative + 2^-126 -- once per closest-hit
+// update, not per node)
+RTW_D float t_lo32(double t) { return (float)widen_lo(t); }
+RTW_D float t_hi32(double t) {
+    const float f = (float)widen_hi(t);
+    return __builtin_fmaf(__builtin_fabsf(f), 0x1p-23f, f) + 0x1p-126f;
+}
 
 // One step of the child-test walks (RTW_CHILD_TEST): the inner node (ca, cb)
 // (its a / b fields) loads both children and slab-tests them together; the
@@ -1031,14 +1107,75 @@ RTW_D bool expand_children(const scene& S, const slab_ray& sr, float t0, float t
     return hn || hf;
 }
 
+// Packet walk of one BVH from a wave-uniform root: the wave walks the tree
+// together.  A node is visited when its box passes the slab test of at least
+// one lane (each lane with its own closest t), so the node index, the stack
+// and the leaf items are wave-uniform: nodes, items and prims come in by
+// scalar loads, the stack is one LDS row per wave, and every lane's slab test
+// runs in the same instruction (a per-lane walk left two thirds of the lanes
+// idle while the wave's longest walk finished).  A leaf's exact tests run on
+// the lanes whose slab test passed (leaf(first, count) is called under that
+// mask).  Inner nodes continue with the child most passing lanes would visit
+// first and stack the other.  Each lane gets its own walk's result: every node
+// its own walk would enter with a given closest t passes its test here with
+// the same or a larger t (t only shrinks), leaves it would skip cannot beat
+// its closest hit, and better() makes the winner independent of the order.
+// Measured (1 MI355X, A/B against the per-lane walks): C3 slice 1 665 vs
+// 2 572 Msamples/s, C5 slice 318 vs 597 (profiles/r03/ab_packet_rejected.log).
+// Every node is one dependent scalar load -> slab test -> ballot -> branch
+// step, ~100 of them per wave-iteration on C3, and four waves per SIMD do
+// not hide that chain; per-lane walks keep 64 loads in flight per
+// instruction.  Off; -DRTW_PACKET=1 / -DRTW_PACKET_GROUP=1 select it.
+#ifndef RTW_PACKET
+#define RTW_PACKET 0  // world BVH walks
+#endif
+#ifndef RTW_PACKET_GROUP
+#define RTW_PACKET_GROUP 0  // group BVH walks from uniform roots
+#endif
+template <class LEAF>
+RTW_D void packet_walk(const scene& S, int root, const slab_ray& sr, float t0, int dneg, const hit_state& h,
+                       uint16_t* ws, LEAF&& leaf) {
+    int wsp = 0;  // wave-uniform
+    int ni = root;
+    for (;;) {
+        const bvh_node32 nd = node_s(S, ni);
+        const bool pass = slab32(nd, sr, t0, t_hi32(h.t));
+        const uint64_t m = __builtin_amdgcn_ballot_w64(pass);
+        if (m) {
+            if (nd.b < 0) {
+                if (pass) leaf(nd.a, -nd.b);
+            } else {
+                const int pad = nd.b >> 28, right = nd.b & 0x0fffffff;
+                const bool lf = (((dneg >> (pad & 3)) ^ (pad >> 2)) & 1) == 0;
+                const uint64_t ml = __builtin_amdgcn_ballot_w64(pass && lf);
+                const bool left_first = 2 * __builtin_popcountll(ml) >= __builtin_popcountll(m);
+                if (wsp < lds_stack::wave_cap)  // always true: depth checked at upload
+                    ws[wsp++] = (uint16_t)(left_first ? right : nd.a);
+                ni = left_first ? nd.a : right;
+                continue;
+            }
+        }
+        if (wsp == 0) break;
+        ni = __builtin_amdgcn_readfirstlane((int)ws[--wsp]);
+    }
+}
+
 // BVH over the prims of one group (items = prim indices).
-template <class STK>
+// PK: the root is wave-uniform and no walk encloses this one (the media
+// walk, the world runs): the packet walk (with LDS stacks).
+template <bool PK = false, class STK>
 RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_state& h, STK& stk, int base,
                      bool movers) {
     const double fc = motion_frac(S, r.t, movers);
     const slab_ray sr = make_slab_ray(S, r);
     const int dneg = dir_mask(r.d);
-    const float t0 = (float)widen_lo(t_min);
+    const float t0 = t_lo32(t_min);
+    if constexpr (PK && RTW_PACKET_GROUP && std::is_same<STK, lds_stack>::value) {
+        packet_walk(S, root, sr, t0, dneg, h, stk.wave_row(), [&](int la, int lc) {
+            for (int k = 0; k < lc; ++k) arbitrate_item_u(S, ld(&S.items[la + k]), r, t_min, h, fc);
+        });
+        return;
+    }
     int sp = base;
 #ifndef RTW_GROUP_WW
 #define RTW_GROUP_WW 1
@@ -1052,7 +1189,7 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
         int la = 0, lc = 0;
         while (lc == 0 && sp > base) {
             const bvh_node32 nd = node_at(S, stk.at(--sp));
-            if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
+            if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
             lc = node_count(nd);
             la = nd.a;
             if (lc == 0 && sp + 2 <= STK::cap) push_children(nd, dneg, stk, sp);
@@ -1064,7 +1201,7 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
     stk.at(sp++) = root;
     while (sp > base) {
         const bvh_node32 nd = node_at(S, stk.at(--sp));
-        if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
+        if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
         const int cnt = node_count(nd);
         if (cnt > 0) {
             for (int k = 0; k < cnt; ++k) arbitrate_item(S, S.items[nd.a + k], r, t_min, h, fc);
@@ -1075,10 +1212,11 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
 #endif
 }
 
+// (called with wave-uniform entries only: the media walk)
 template <int F, class STK>
 RTW_D void group_closest(const scene& S, const entry_v& e, const ray& r, double t_min, hit_state& h, STK& stk) {
     if ((F & F_GBVH) && e.bvh_root >= 0)
-        group_bvh(S, e.bvh_root, r, t_min, h, stk, 0, e.movers);
+        group_bvh<true>(S, e.bvh_root, r, t_min, h, stk, 0, e.movers);
     else
         group_scan(S, e.first_prim, e.n_prims, r, t_min, h, e.movers);
 }
@@ -1136,7 +1274,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
         const double fc = motion_frac(S, r.t, S.mv_common != 0);  // transforms keep the ray's time
         const slab_ray sr = make_slab_ray(S, r);
         const int dneg = dir_mask(r.d);
-        const float t0 = (float)widen_lo(kTMin);
+        const float t0 = t_lo32(kTMin);
         int sp = 0;
         stk.at(sp++) = S.world_bvh_root;
         // Leaf items: prims (~prim) or entries (their groups, flat or BVH)
@@ -1165,6 +1303,24 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                 }
             }
         };
+        if constexpr ((F & F_GBVH) == 0 && RTW_PACKET && std::is_same<STK, lds_stack>::value) {
+            // the packet walk (packet_walk); leaf items are prims (~prim) or
+            // entries, wave-uniform
+            packet_walk(S, S.world_bvh_root, sr, t0, dneg, h, stk.wave_row(), [&](int la, int lc) {
+                for (int k = 0; k < lc; ++k) {
+                    const int it = ld(&S.items[la + k]);
+                    if (it < 0) {  // plain one-prim entry
+                        arbitrate_u(S, ~it, r, kTMin, h, fc, ya, oka);
+                        continue;
+                    }
+                    const entry_v e = view_entry<true>(S, it);
+                    const ray lr = entry_local_ray<true>(e, r);
+                    for (int i = 0; i < e.n_prims; ++i)
+                        arbitrate_u(S, e.first_prim + i, lr, kTMin, h, fc, 0.0, false);  // exact quotients
+                }
+            });
+            return h;
+        }
         if constexpr ((F & F_GBVH) == 0 && RTW_CHILD_TEST) {
             // Children tested by their parent's iteration: expanding an inner
             // node loads both children and slab-tests them together; a lane
@@ -1177,7 +1333,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             bool have = false;
             {
                 const bvh_node32 rt = node_at(S, S.world_bvh_root);
-                if (slab32(rt, sr, t0, (float)widen_hi(h.t))) ca = rt.a, cb = rt.b, have = true;
+                if (slab32(rt, sr, t0, t_hi32(h.t))) ca = rt.a, cb = rt.b, have = true;
             }
             sp = 0;
             for (;;) {
@@ -1186,14 +1342,14 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                     if (!have) {
                         if (sp == 0) break;
                         const bvh_node32 nd = node_at(S, stk.at(--sp));
-                        if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
+                        if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
                         ca = nd.a, cb = nd.b, have = true;
                     }
                     if (cb < 0) {  // a leaf
                         la = ca, lc = -cb, have = false;
                         break;
                     }
-                    have = expand_children(S, sr, t0, (float)widen_hi(h.t), dneg, stk, sp, ca, cb);
+                    have = expand_children(S, sr, t0, t_hi32(h.t), dneg, stk, sp, ca, cb);
                 }
                 if (lc == 0) break;
                 leaf(la, lc);
@@ -1211,7 +1367,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                 int la = 0, lc = 0;  // this lane's pending leaf: first item, count
                 while (lc == 0 && sp > 0) {
                     const bvh_node32 nd = node_at(S, stk.at(--sp));
-                    if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
+                    if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
                     lc = node_count(nd);
                     la = nd.a;
                     if (lc == 0 && sp + 2 <= STK::cap)  // always true: depth checked at upload
@@ -1223,7 +1379,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
         } else {
             while (sp > 0) {
                 const bvh_node32 nd = node_at(S, stk.at(--sp));
-                if (!slab32(nd, sr, t0, (float)widen_hi(h.t))) continue;
+                if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
                 const int cnt = node_count(nd);
                 if (cnt > 0) {
                     leaf(nd.a, cnt);
@@ -1278,7 +1434,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                     const entry_v e = view_entry<true>(S, ei);
                     lr = entry_local_ray<true>(e, r);
                     if ((F & F_GBVH) && e.bvh_root >= 0) {
-                        group_bvh(S, e.bvh_root, lr, kTMin, h, stk, 0, e.movers);
+                        group_bvh<true>(S, e.bvh_root, lr, kTMin, h, stk, 0, e.movers);
                         continue;
                     }
                 }
