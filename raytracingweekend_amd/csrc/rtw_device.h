@@ -215,7 +215,7 @@ struct dev_entry {
     int32_t phase_material, bvh_root;
     int32_t n_outer_ops;  // MEDIUM: ops enclosing the medium (rtw_entry::n_outer_ops)
     int32_t movers;       // the group holds DP_MOVING_COMMON* spheres
-    int32_t pad;
+    int32_t bvh_root4;    // its BVH as 4-wide nodes (scene::nodes4), -1 none
     double density;
 };
 struct dev_op {
@@ -259,6 +259,14 @@ struct scene {
     const bvh_node32* lnodes;
     int32_t n_lnodes;
     int32_t n_nodes;  // device BVH nodes in all
+    // The same BVHs with 4-wide nodes (bvh_node4, rtw_scene_upload collapses
+    // the binary trees), walked by the persistent kernels with LDS stacks;
+    // nodes4 numbered breadth-first from all roots together like the binary
+    // ones, the top n_lnodes4 staged in LDS (lnodes4).  n_nodes4 = 0: none.
+    const struct bvh_node4* nodes4;
+    const int32_t* leaf4;  // per 4-wide leaf slot: first item | (count << 24)
+    const struct bvh_node4* lnodes4;
+    int32_t n_nodes4, n_lnodes4, world_root4;
 };
 
 // Scene features a traversal kernel is specialised for.
@@ -312,7 +320,7 @@ RTW_D T rd(const T* p) {
 struct entry_v {
     const dev_entry* p;
     const dev_op* ops;  // its op chain
-    int kind, first_prim, n_prims, n_ops, bvh_root;
+    int kind, first_prim, n_prims, n_ops, bvh_root, bvh_root4;
     bool movers;  // the group holds DP_MOVING_COMMON* spheres (dev_entry::movers)
 };
 template <bool U>
@@ -326,6 +334,7 @@ RTW_D entry_v view_entry(const scene& S, int i) {
     e.n_prims = rd<U>(&E[i].n_prims);
     e.n_ops = rd<U>(&E[i].n_ops);
     e.bvh_root = rd<U>(&E[i].bvh_root);
+    e.bvh_root4 = rd<U>(&E[i].bvh_root4);
     e.movers = rd<U>(&E[i].movers) != 0;
     return e;
 }
@@ -1000,7 +1009,20 @@ RTW_D bool slab32(const bvh_node32& nd, const slab_ray& s, float t0, float t1) {
 // a world-BVH leaf) share one stack above the outer walk's entries; the host
 // checks at upload that the deepest nesting fits (rtw_scene_upload).
 constexpr int kStack = 48;
-constexpr int kLdsStack = 16;
+// Measured (1 MI355X, A/B against the binary child-test / while-while
+// walks, profiles/r03/ab_bvh4_rejected.log): C3 slice 2 592 vs 2 611
+// Msamples/s, C5 slice 545 vs 599.  On C3 it issues 8.6 % fewer VALU and
+// 15 % fewer SALU / LDS instructions per segment but 40 % more global
+// loads (a 4-wide node is 112 bytes: the LDS packet holds three levels
+// instead of eight) and 15 % more issue stalls, for the same time; the C5
+// kernel spills 25 VGPRs (6 before).  Off; -DRTW_BVH4=1 selects it.
+#ifndef RTW_BVH4
+#define RTW_BVH4 0
+#endif
+#ifndef RTW_LDS_STACK
+#define RTW_LDS_STACK (RTW_BVH4 ? 20 : 16)  // 4-wide walks push up to three children per level
+#endif
+constexpr int kLdsStack = RTW_LDS_STACK;
 struct local_stack {
     static constexpr int cap = kStack;
     int s[kStack];
@@ -1038,6 +1060,42 @@ RTW_D bvh_node32 node_at(const scene& S, int i) {
     bvh_node32 nd;
     __builtin_memcpy(&nd, &a, 16);
     __builtin_memcpy(reinterpret_cast<char*>(&nd) + 16, &b, 16);
+    return nd;
+}
+
+// 4-wide BVH node (rtw_scene_upload collapses each binary tree: a node's
+// slots are its binary children, the largest-area inner ones opened once
+// more until there are four), bounds per axis for the four slots so each
+// 16-byte load brings one plane of all four boxes (and pairs of slots sit in
+// adjacent registers for the packed fp32 slab test).  child[c] >= 0: inner
+// node4; kNoChild: an unused slot; other values < 0: leaf ~l
+// (scene::leaf4[l]).  The walks read the first 112 bytes.
+constexpr int32_t kNoChild = INT32_MIN;
+struct bvh_node4 {
+    float lo[3][4], hi[3][4];
+    int32_t child[4];
+    int32_t pad[4];
+};
+static_assert(sizeof(bvh_node4) == 128, "bvh_node4 layout");
+
+RTW_D bvh_node4 node4_at(const scene& S, int i) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    using lds_v4 = const __attribute__((address_space(3))) v4u;
+    using glb_v4 = const __attribute__((address_space(1))) v4u;
+    v4u a[7];
+    if (i < S.n_lnodes4) {
+        lds_v4* p = (lds_v4*)(S.lnodes4 + i);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) a[k] = p[k];
+    } else {
+        glb_v4* p = (glb_v4*)(S.nodes4 + i);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) a[k] = p[k];
+        asm volatile("" ::"v"(a[0].x));  // global loads, not one flat load (node_at)
+    }
+    bvh_node4 nd;
+    __builtin_memcpy(&nd, a, 112);
+    nd.pad[0] = nd.pad[1] = nd.pad[2] = nd.pad[3] = 0;
     return nd;
 }
 
@@ -1107,6 +1165,96 @@ RTW_D bool expand_children(const scene& S, const slab_ray& sr, float t0, float t
     return hn || hf;
 }
 
+// slab32 for the four slots of a bvh_node4 at once: the near / far plane
+// values of slot pairs {0, 1} and {2, 3} come from packed fp32 fmas (one
+// v_pk_fma_f32 per two slots, the same IEEE operation per slot as slab32's,
+// so its conservative bound holds per slot); tn[c] is the slot's entry t.
+RTW_D void slab4(const bvh_node4& nd, const slab_ray& s, float t0, float t1, float tn[4], bool pass[4]) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 n01 = t0, n23 = t0, f01 = t1, f23 = t1;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const f2 inv = s.inv[k], oin = s.oin[k], oif = s.oif[k];
+        const f2 lo01 = {nd.lo[k][0], nd.lo[k][1]}, lo23 = {nd.lo[k][2], nd.lo[k][3]};
+        const f2 hi01 = {nd.hi[k][0], nd.hi[k][1]}, hi23 = {nd.hi[k][2], nd.hi[k][3]};
+        const f2 an01 = __builtin_elementwise_fma(lo01, inv, oin), bn01 = __builtin_elementwise_fma(hi01, inv, oin);
+        const f2 af01 = __builtin_elementwise_fma(lo01, inv, oif), bf01 = __builtin_elementwise_fma(hi01, inv, oif);
+        const f2 an23 = __builtin_elementwise_fma(lo23, inv, oin), bn23 = __builtin_elementwise_fma(hi23, inv, oin);
+        const f2 af23 = __builtin_elementwise_fma(lo23, inv, oif), bf23 = __builtin_elementwise_fma(hi23, inv, oif);
+        n01 = __builtin_elementwise_max(n01, __builtin_elementwise_min(an01, bn01));
+        n23 = __builtin_elementwise_max(n23, __builtin_elementwise_min(an23, bn23));
+        f01 = __builtin_elementwise_min(f01, __builtin_elementwise_max(af01, bf01));
+        f23 = __builtin_elementwise_min(f23, __builtin_elementwise_max(af23, bf23));
+    }
+    tn[0] = n01.x, tn[1] = n01.y, tn[2] = n23.x, tn[3] = n23.y;
+    pass[0] = n01.x <= f01.x && nd.child[0] != kNoChild;
+    pass[1] = n01.y <= f01.y && nd.child[1] != kNoChild;
+    pass[2] = n23.x <= f23.x && nd.child[2] != kNoChild;
+    pass[3] = n23.y <= f23.y && nd.child[3] != kNoChild;
+}
+
+// Walk of a 4-wide BVH from node4 `root` (its own box is not tested: its
+// slots are), while-while as the binary walks: every lane expands nodes --
+// continuing with its nearest passing slot, stacking the other passing ones
+// -- until it holds a leaf (or its stack runs dry), then all lanes test their
+// leaves together with leaf(first_item, count).  Stacked slots are not
+// re-tested when popped (the leaf tests and the next expansion cull with the
+// closest t of that time).  The stack above `base` holds node4 indices and
+// ~leaf (16-bit: upload checks both spaces and the depth).  Visiting order
+// never changes a lane's result: better() (arbitrate) reproduces the list
+// order's tie rule.
+template <class STK, class LEAF>
+RTW_D void walk4(const scene& S, int root, const slab_ray& sr, float t0, const hit_state& h, STK& stk, int base,
+                 LEAF&& leaf) {
+    int sp = base;
+    int cur = root;  // the node4 this lane expands next, -1: pop one
+    for (;;) {
+        int la = 0, lc = 0;  // this lane's pending leaf
+        while (lc == 0) {
+            int lf = -1;  // a leaf reached: its leaf4 index
+            if (cur < 0) {
+                if (sp == base) break;
+                const int e = (int16_t)stk.at(--sp);
+                if (e >= 0)
+                    cur = e;
+                else
+                    lf = ~e;
+            }
+            if (cur >= 0) {
+                const bvh_node4 nd = node4_at(S, cur);
+                float tn[4];
+                bool pass[4];
+                slab4(nd, sr, t0, t_hi32(h.t), tn, pass);
+                int best = -1;
+                float bt = __builtin_inff();
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (pass[c] && tn[c] < bt) best = c, bt = tn[c];
+                // the others, farthest slot last pushed ... popped first
+#pragma unroll
+                for (int c = 3; c >= 0; --c)
+                    if (pass[c] && c != best && sp < STK::cap)  // always fits: depth checked at upload
+                        stk.at(sp++) = (uint16_t)nd.child[c];
+                cur = -1;
+                if (best >= 0) {
+                    const int ch = best == 0 ? nd.child[0] : best == 1 ? nd.child[1] : best == 2 ? nd.child[2] : nd.child[3];
+                    if (ch >= 0)
+                        cur = ch;
+                    else
+                        lf = ~ch;
+                }
+            }
+            if (lf >= 0) {
+                const int v = S.leaf4[lf];
+                la = v & 0xffffff;
+                lc = v >> 24;
+            }
+        }
+        if (lc == 0) break;
+        leaf(la, lc);
+    }
+}
+
 // Packet walk of one BVH from a wave-uniform root: the wave walks the tree
 // together.  A node is visited when its box passes the slab test of at least
 // one lane (each lane with its own closest t), so the node index, the stack
@@ -1164,12 +1312,18 @@ RTW_D void packet_walk(const scene& S, int root, const slab_ray& sr, float t0, i
 // PK: the root is wave-uniform and no walk encloses this one (the media
 // walk, the world runs): the packet walk (with LDS stacks).
 template <bool PK = false, class STK>
-RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_state& h, STK& stk, int base,
-                     bool movers) {
+RTW_D void group_bvh(const scene& S, int root, int root4, const ray& r, double t_min, hit_state& h, STK& stk,
+                     int base, bool movers) {
     const double fc = motion_frac(S, r.t, movers);
     const slab_ray sr = make_slab_ray(S, r);
     const int dneg = dir_mask(r.d);
     const float t0 = t_lo32(t_min);
+    if constexpr (RTW_BVH4 && std::is_same<STK, lds_stack>::value) {
+        walk4(S, root4, sr, t0, h, stk, base, [&](int la, int lc) {
+            for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
+        });
+        return;
+    }
     if constexpr (PK && RTW_PACKET_GROUP && std::is_same<STK, lds_stack>::value) {
         packet_walk(S, root, sr, t0, dneg, h, stk.wave_row(), [&](int la, int lc) {
             for (int k = 0; k < lc; ++k) arbitrate_item_u(S, ld(&S.items[la + k]), r, t_min, h, fc);
@@ -1216,7 +1370,7 @@ RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_s
 template <int F, class STK>
 RTW_D void group_closest(const scene& S, const entry_v& e, const ray& r, double t_min, hit_state& h, STK& stk) {
     if ((F & F_GBVH) && e.bvh_root >= 0)
-        group_bvh<true>(S, e.bvh_root, r, t_min, h, stk, 0, e.movers);
+        group_bvh<true>(S, e.bvh_root, e.bvh_root4, r, t_min, h, stk, 0, e.movers);
     else
         group_scan(S, e.first_prim, e.n_prims, r, t_min, h, e.movers);
 }
@@ -1297,7 +1451,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                 const entry_v e = view_entry<false>(S, it);
                 const ray lr = entry_local_ray<false>(e, r);
                 if ((F & F_GBVH) && e.bvh_root >= 0) {
-                    group_bvh(S, e.bvh_root, lr, kTMin, h, stk, sp, S.mv_common != 0);
+                    group_bvh(S, e.bvh_root, e.bvh_root4, lr, kTMin, h, stk, sp, S.mv_common != 0);
                 } else {
                     for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMin, h, fc);
                 }
@@ -1319,6 +1473,10 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                         arbitrate_u(S, e.first_prim + i, lr, kTMin, h, fc, 0.0, false);  // exact quotients
                 }
             });
+            return h;
+        }
+        if constexpr ((F & F_GBVH) == 0 && RTW_BVH4 && std::is_same<STK, lds_stack>::value) {
+            walk4(S, S.world_root4, sr, t0, h, stk, 0, leaf);
             return h;
         }
         if constexpr ((F & F_GBVH) == 0 && RTW_CHILD_TEST) {
@@ -1434,7 +1592,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                     const entry_v e = view_entry<true>(S, ei);
                     lr = entry_local_ray<true>(e, r);
                     if ((F & F_GBVH) && e.bvh_root >= 0) {
-                        group_bvh<true>(S, e.bvh_root, lr, kTMin, h, stk, 0, e.movers);
+                        group_bvh<true>(S, e.bvh_root, e.bvh_root4, lr, kTMin, h, stk, 0, e.movers);
                         continue;
                     }
                 }

@@ -732,10 +732,10 @@ void k_persist(persist_args) {
     }
     if (LST) {  // the BVH node packet (the top levels of every tree)
         const persist_args& A = args_now();
-        const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
+        const uint4* src = reinterpret_cast<const uint4*>(RTW_BVH4 ? (const void*)A.S.nodes4 : (const void*)A.S.nodes);
         uint4* dst = reinterpret_cast<uint4*>(s_scene + A.lds_nodes_off);
-        for (uint32_t k = threadIdx.x; k < A.lds_nodes * (uint32_t)(sizeof(bvh_node32) / 16); k += kBlock)
-            dst[k] = src[k];
+        constexpr uint32_t kNode16 = (uint32_t)((RTW_BVH4 ? sizeof(bvh_node4) : sizeof(bvh_node32)) / 16);
+        for (uint32_t k = threadIdx.x; k < A.lds_nodes * kNode16; k += kBlock) dst[k] = src[k];
     }
     if (LDS || LST) __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
@@ -903,8 +903,13 @@ void k_persist(persist_args) {
             scene S = A.S;
             hit_state h;
             if constexpr (LST) {
-                S.lnodes = reinterpret_cast<const bvh_node32*>(s_scene + A.lds_nodes_off);
-                S.n_lnodes = (int32_t)A.lds_nodes;
+                if constexpr (RTW_BVH4) {
+                    S.lnodes4 = reinterpret_cast<const bvh_node4*>(s_scene + A.lds_nodes_off);
+                    S.n_lnodes4 = (int32_t)A.lds_nodes;
+                } else {
+                    S.lnodes = reinterpret_cast<const bvh_node32*>(s_scene + A.lds_nodes_off);
+                    S.n_lnodes = (int32_t)A.lds_nodes;
+                }
                 lds_stack stk{&s_stack[0][tid]};
                 h = world_closest<F>(S, x.r, x.rng, stk);
             } else {
@@ -1780,6 +1785,7 @@ struct handle_t {
     int grid = 2048;
     int cus = 256;
     int stack_need = 0;  // deepest BVH stack a traversal of this scene can use
+    int stack4_need = INT32_MAX;  // ... with 4-wide walks (INT32_MAX: no 4-wide BVH)
     // BVH boxes of moving spheres cover the desc camera's shutter only
     bool bvh_motion = false;
     double shutter0 = 0.0, shutter1 = 0.0;
@@ -2084,6 +2090,93 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         for (rtw_entry& E : dentries)
             if (E.bvh_root >= 0) E.bvh_root = newid[E.bvh_root];
     }
+    // 4-wide BVHs (rtw_device.h bvh_node4, walk4) collapsed from the binary
+    // device trees: a node4's slots are the binary node's children, the
+    // inner slot with the largest surface area opened again (replaced in
+    // place by its two children) until there are four or only leaves are
+    // left.  Numbered breadth-first from all roots together (the LDS packet
+    // takes the first ones); leaves become leaf4 records (first item | count
+    // << 24).  A binary root that is a leaf gets a node4 of one slot.
+    std::vector<bvh_node4> n4;
+    std::vector<int32_t> leaf4;
+    std::vector<int> root4_of(dnodes32.size(), -1);  // binary root -> node4
+    int world_root4 = -1, depth4_world = 0, depth4_group = 0;
+    bool bvh4_ok = RTW_BVH4 && bvh_ok && !dnodes32.empty();
+    if (bvh4_ok) {
+        auto is_leaf = [&](int b) { return dnodes32[b].b < 0; };
+        auto area = [&](int b) {
+            const bvh_node32& N = dnodes32[b];
+            const double x = (double)N.hi[0] - N.lo[0], y = (double)N.hi[1] - N.lo[1], z = (double)N.hi[2] - N.lo[2];
+            return x * y + y * z + z * x;
+        };
+        std::vector<std::pair<int, int>> q;  // (binary node, depth4) in BFS order; node4 id = position
+        auto add_root = [&](int b) {
+            if (b < 0) return -1;
+            if (root4_of[b] >= 0) return root4_of[b];
+            root4_of[b] = (int)q.size();
+            q.push_back({b, 1});
+            return root4_of[b];
+        };
+        world_root4 = add_root(world_root);
+        for (const rtw_entry& E : dentries) add_root(E.bvh_root);
+        n4.reserve(dnodes32.size());
+        for (size_t qi = 0; qi < q.size(); ++qi) {
+            const int b = q[qi].first, dep = q[qi].second;
+            std::vector<int> slots;
+            if (is_leaf(b)) {
+                slots.push_back(b);
+            } else {
+                slots = {dnodes32[b].a, dnodes32[b].b & 0x0fffffff};
+                while (slots.size() < 4) {
+                    int pick = -1;
+                    double best = -1.0;
+                    for (size_t k = 0; k < slots.size(); ++k)
+                        if (!is_leaf(slots[k]) && area(slots[k]) > best) best = area(slots[k]), pick = (int)k;
+                    if (pick < 0) break;
+                    const bvh_node32& N = dnodes32[slots[pick]];
+                    slots[pick] = N.a;
+                    slots.insert(slots.begin() + pick + 1, N.b & 0x0fffffff);
+                }
+            }
+            bvh_node4 M;
+            std::memset(&M, 0, sizeof M);
+            for (int c = 0; c < 4; ++c) {
+                if (c >= (int)slots.size()) {  // unused slot: never passes (slab4)
+                    M.child[c] = kNoChild;
+                    continue;
+                }
+                const bvh_node32& N = dnodes32[slots[c]];
+                for (int k = 0; k < 3; ++k) M.lo[k][c] = N.lo[k], M.hi[k][c] = N.hi[k];
+                if (N.b < 0) {
+                    bvh4_ok = bvh4_ok && N.a < (1 << 24) && -N.b < 128;
+                    M.child[c] = ~(int32_t)leaf4.size();
+                    leaf4.push_back(N.a | (-N.b << 24));
+                } else {
+                    M.child[c] = (int32_t)q.size();
+                    q.push_back({slots[c], dep + 1});
+                }
+            }
+            n4.push_back(M);
+        }
+        // depth of every 4-wide tree (the stack bound below)
+        std::vector<int> d4(n4.size(), 0);
+        for (size_t i = 0; i < q.size(); ++i) d4[i] = q[i].second;
+        std::vector<int> owner(n4.size(), -1);  // root node4 of each node4
+        for (size_t i = 0; i < n4.size(); ++i) {
+            if (owner[i] < 0) owner[i] = (int)i;
+            for (int c = 0; c < 4; ++c)
+                if (n4[i].child[c] >= 0) owner[n4[i].child[c]] = owner[i];
+        }
+        for (size_t i = 0; i < n4.size(); ++i) {
+            const int dd = d4[i] - d4[owner[i]] + 1;
+            if (owner[i] == world_root4)
+                depth4_world = std::max(depth4_world, dd);
+            else
+                depth4_group = std::max(depth4_group, dd);
+        }
+        // 16-bit LDS stack entries: node4 ids >= 0, ~leaf < 0
+        bvh4_ok = bvh4_ok && n4.size() < 32768 && leaf4.size() < 32768;
+    }
     // device entries (dev_entry) and their op pool
     std::vector<dev_entry> dev_entries(std::max<size_t>(dentries.size(), 1));
     std::vector<dev_op> dev_ops;
@@ -2095,6 +2188,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         D.first_op = (int32_t)dev_ops.size();
         D.phase_material = E.phase_material, D.bvh_root = E.bvh_root, D.n_outer_ops = E.n_outer_ops;
         D.movers = entry_movers[e];
+        D.bvh_root4 = (bvh4_ok && E.bvh_root >= 0) ? root4_of[E.bvh_root] : -1;
         D.density = E.density;
         for (int k = 0; k < E.n_ops; ++k) {
             dev_op o;
@@ -2123,6 +2217,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {ditems.data(), sizeof(int32_t) * ditems.size(), 0},
         {runs.data(), sizeof(world_run) * runs.size(), 0},
         {ysph.data(), sizeof(float) * ysph.size(), 0},
+        {n4.data(), sizeof(bvh_node4) * n4.size(), 0},
+        {leaf4.data(), sizeof(int32_t) * leaf4.size(), 0},
     };
     size_t total = 0;
     for (auto& p : parts) {
@@ -2154,6 +2250,12 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.items = (const int32_t*)at(12);
     S.runs = (const world_run*)at(13);
     S.ysph = (const float*)at(14);
+    S.nodes4 = bvh4_ok ? (const bvh_node4*)at(15) : nullptr;
+    S.leaf4 = bvh4_ok ? (const int32_t*)at(16) : nullptr;
+    S.n_nodes4 = bvh4_ok ? (int32_t)n4.size() : 0;
+    S.world_root4 = bvh4_ok ? world_root4 : -1;
+    S.lnodes4 = nullptr;
+    S.n_lnodes4 = 0;
     S.ysb_cx = ysb[0], S.ysb_cy = ysb[1], S.ysb_dy = ysb[2], S.ysb_cz = ysb[3], S.ysb_r2 = ysb[4];
     S.n_runs = (int32_t)runs.size();
     S.mv_common = mv_common ? 1 : 0;
@@ -2226,6 +2328,15 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         if (d->entries[e].bvh_root >= 0) group_depth = std::max(group_depth, depth(d->entries[e].bvh_root));
     const int world_depth = d->world_bvh_root >= 0 ? depth(d->world_bvh_root) : 0;
     h->stack_need = world_depth + group_depth + 2;
+    // 4-wide walks (walk4) stack up to three slots per level; a group walk
+    // nested in a world-BVH leaf (F_WBVH | F_GBVH) sits on the binary world
+    // walk's entries
+    {
+        const bool nested = d->world_bvh_root >= 0 && (h->features & F_GBVH);
+        const int world4 = d->world_bvh_root < 0 ? 0 : nested ? world_depth + 1 : 3 * depth4_world + 1;
+        const int group4 = (h->features & F_GBVH) ? 3 * depth4_group + 1 : 0;
+        h->stack4_need = bvh4_ok ? world4 + group4 + 1 : INT32_MAX;
+    }
     bool movers = false;
     for (int k = 0; k < d->n_prims; ++k) movers |= d->prims[k].type == RTW_PRIM_MOVING_SPHERE;
     h->bvh_motion = movers && d->n_bvh_nodes > 0;
@@ -2454,6 +2565,8 @@ bool sort_forced(bool& value) {
 // A/B).  The node count of the last launch or probe is kept for
 // rtw_scene_query.
 thread_local uint32_t g_node_packet = 0;
+// the packet holds 4-wide nodes when the walks are 4-wide (RTW_BVH4)
+constexpr size_t kPacketNodeBytes = RTW_BVH4 ? sizeof(bvh_node4) : sizeof(bvh_node32);
 template <int FF, int MM, bool LL>
 uint32_t node_packet(size_t shm, int n_nodes) {
     const char* e = std::getenv("RTW_LDS_NODES");
@@ -2466,7 +2579,7 @@ uint32_t node_packet(size_t shm, int n_nodes) {
     uint32_t best = 0;
     for (uint32_t k = 32; k <= cap + 31; k += 32) {
         const uint32_t kk = std::min(k, cap);
-        if (blocks_per_cu(fn, kBlock, off + kk * sizeof(bvh_node32)) < base) break;
+        if (blocks_per_cu(fn, kBlock, off + kk * kPacketNodeBytes) < base) break;
         best = kk;
         if (kk == cap) break;
     }
@@ -2486,12 +2599,13 @@ void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t s
         if (!probe)
             hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)),
                                dim3(kSortBlock), shm, st, persist_args{S, J, C, base, bytes});
-    } else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack && S.n_nodes < 65536) {  // 16-bit LDS stacks
+    } else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack &&
+               (RTW_BVH4 ? S.n_nodes4 > 0 : S.n_nodes < 65536)) {  // 16-bit LDS stacks
         if (name) *name = kname("k_persist", FF, MM, LL, true);
-        const uint32_t packet = node_packet<FF, MM, LL>(shm, S.n_nodes);
+        const uint32_t packet = node_packet<FF, MM, LL>(shm, RTW_BVH4 ? S.n_nodes4 : S.n_nodes);
         const uint32_t off = (uint32_t)((shm + 15) & ~size_t(15));
         g_node_packet = packet;
-        const size_t shm2 = packet ? off + packet * sizeof(bvh_node32) : shm;
+        const size_t shm2 = packet ? off + packet * kPacketNodeBytes : shm;
         if (!probe)
             hipLaunchKernelGGL((k_persist<FF, MM, LL, true>), dim3(persist_grid<FF, MM, LL, true>(shm, cus)),
                                dim3(kBlock), shm2, st, persist_args{S, J, C, base, bytes, packet, off});
@@ -2588,6 +2702,9 @@ bool fast_sort_enabled() {
     }();
     return on;
 }
+// the stack a persistent fp64 launch with LDS stacks needs: the 4-wide
+// walks' (RTW_BVH4) or the binary ones'
+int lst_stack_need(const handle_t* h) { return RTW_BVH4 ? h->stack4_need : h->stack_need; }
 void launch_fast(bool probe, const handle_t* h, hipStream_t st, const fast_args& A, std::string* name = nullptr) {
     const int f = h->features & (F_MEDIA | F_WBVH | F_GBVH);
     if ((f & (F_WBVH | F_GBVH)) == 0 && fast_sort_enabled()) {  // list scenes: regrouping kernel
@@ -2821,7 +2938,7 @@ std::string render_kernel_name(const handle_t* h) {
     const char* mode_env = std::getenv("RTW_MODE");
     const bool wavefront = mode_env && std::string(mode_env) == "wavefront";
     if (!wavefront && launch_persist(true, h->features, h->shade_mask, 0, nullptr, h->S, J, nullptr, h->scene_base,
-                                     h->shade_bytes, h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0,
+                                     h->shade_bytes, lst_stack_need(h), h->ysph, !h->movers, h->S.n_lights > 0,
                                      h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL,
                                      &name))
         return name;
@@ -3110,7 +3227,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     }
     const bool persistent = fast || (!(mode_env && std::string(mode_env) == "wavefront") &&
                                      launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J, C,
-                                                    h->scene_base, h->shade_bytes, h->stack_need, h->ysph, !h->movers,
+                                                    h->scene_base, h->shade_bytes, lst_stack_need(h), h->ysph, !h->movers,
                                                     h->S.n_lights > 0,
                                                     h->S.background != RTW_BG_GRADIENT &&
                                                         h->S.render_type != RTW_RENDER_NORMAL));
@@ -3134,7 +3251,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 launch_fast(false, h, st, FA);
             } else {
                 launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base,
-                               h->shade_bytes, h->stack_need, h->ysph, !h->movers, h->S.n_lights > 0,
+                               h->shade_bytes, lst_stack_need(h), h->ysph, !h->movers, h->S.n_lights > 0,
                                h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL);
             }
             HIPCHK(hipGetLastError());
