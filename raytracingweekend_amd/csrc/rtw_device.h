@@ -569,6 +569,62 @@ RTW_D bool rect_t_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, doubl
 #define RTW_RECT_RCP 1
 #endif
 
+// Two consecutive rects of a world run in parallel planes with the same
+// bounds (rtw_scene_upload marks the first with kRectPairHead: Cornell's
+// side walls, its ceiling and floor), in list order with the reference's
+// tests (hittable.h:149-257).  A plane whose quotient t = (k - o.K) / d.K
+// cannot reach t_min = 0.001 -- k - o.K of the other sign than d.K, or
+// |k - o.K| <= 0.00099 |d.K| -- is rejected by the range test whatever its
+// bounds, so a lane needs only the planes ahead of it: for an origin between
+// the planes (a ray inside the room) exactly one.  Every lane tests its one
+// plane in one instruction stream (same quotient, bounds test and
+// acceptance as rect_axis_rcp); lanes that need both (origin outside the
+// pair's slab) or whose d.K is 0 or not finite (a 0 / 0 quotient passes the
+// reference's range test) test both planes in list order in a branch that a
+// wave skips when none of its lanes needs it.  Two planes with distinct k
+// never give a lane equal t, so the winner is the list order's.
+// Measured (1 MI355X, A/B, profiles/r03/ab_rect_pairs_rejected.log): T
+// 4 243 vs 4 430 Msamples/s -- two of the twelve rect tests fewer, but the
+// pair's selects and branch raise the kernel's SGPR spills from 12 to 46.
+// Off; -DRTW_RECT_PAIRS=1 selects it.
+#ifndef RTW_RECT_PAIRS
+#define RTW_RECT_PAIRS 0
+#endif
+constexpr int32_t kRectPairHead = 0x40000000;  // in rtw_prim::flip (device copy only)
+template <int K, int A, int B>
+RTW_D void rect_pair_rcp(const rtw_prim& qa, const rtw_prim& qb, int ia, const ray& r, const rect_rcp& rr,
+                         double t_min, hit_state& h) {
+    const double oK = K == 0 ? r.o.x : (K == 1 ? r.o.y : r.o.z);
+    const double dK = K == 0 ? r.d.x : (K == 1 ? r.d.y : r.d.z);
+    const double na = qa.p[4] - oK, nb = qb.p[4] - oK;
+    const double lim = 0.00099 * __builtin_fabs(dK);
+    const bool ahead_a = ((na > 0 && dK > 0) || (na < 0 && dK < 0)) && __builtin_fabs(na) > lim;
+    const bool ahead_b = ((nb > 0 && dK > 0) || (nb < 0 && dK < 0)) && __builtin_fabs(nb) > lim;
+    const bool both = (ahead_a && ahead_b) || !(__builtin_fabs(dK) > 0 && __builtin_fabs(dK) < __builtin_inf()) ||
+                      na != na || nb != nb;  // a NaN origin: the reference accepts its NaN quotients
+    double t;
+    if (!both) {
+        rtw_prim qs = qa;  // the plane ahead (a when neither is: rejected by its range test)
+        qs.p[4] = ahead_b ? qb.p[4] : qa.p[4];
+        if (rect_axis_rcp<K, A, B>(qs, r, rr, t_min, h.t, t)) {
+            h.t = t;
+            h.prim = ahead_b ? ia + 1 : ia;
+            h.rect = true;
+        }
+    } else {
+        if (rect_axis_rcp<K, A, B>(qa, r, rr, t_min, h.t, t)) {
+            h.t = t;
+            h.prim = ia;
+            h.rect = true;
+        }
+        if (rect_axis_rcp<K, A, B>(qb, r, rr, t_min, h.t, t)) {
+            h.t = t;
+            h.prim = ia + 1;
+            h.rect = true;
+        }
+    }
+}
+
 // Linear closest hit over prims [first, first+n) of one group, in list order
 // (t range (t_min, closest]) with the reference's own comparisons; the
 // primitive data are wave-uniform scalar loads.
@@ -604,6 +660,16 @@ RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_m
                     h.rect = false;
                 }
             }
+        } else if (kRcp && RTW_RECT_PAIRS && (q.flip & kRectPairHead)) {
+            // rects first + i, first + i + 1: parallel, the same bounds
+            const rtw_prim q2 = uprim(S.prims, first + i + 1);
+            if (q.type == RTW_PRIM_RECT_XY)
+                rect_pair_rcp<2, 0, 1>(q, q2, first + i, r, rr, t_min, h);
+            else if (q.type == RTW_PRIM_RECT_XZ)
+                rect_pair_rcp<1, 0, 2>(q, q2, first + i, r, rr, t_min, h);
+            else
+                rect_pair_rcp<0, 1, 2>(q, q2, first + i, r, rr, t_min, h);
+            ++i;
         } else {
             double t;
             if (kRcp ? rect_t_rcp(q, r, rr, t_min, h.t, t) : rect_t(q, r, t_min, h.t, t)) {

@@ -1951,6 +1951,24 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         for (int i = R.first_prim; i < R.first_prim + R.n_prims; ++i)
             if (dprims[i].type == RTW_PRIM_SPHERE) dprims[i].p[5] = 0.0;
     }
+    // rect pairs of plain runs (rtw_device.h rect_pair_rcp): consecutive
+    // rects of one type with the same bounds in different planes
+    if (RTW_RECT_PAIRS) {
+        for (const world_run& R : runs) {
+            if (R.entry != WORLD_RUN_PLAIN) continue;
+            for (int i = R.first_prim; i + 1 < R.first_prim + R.n_prims; ++i) {
+                rtw_prim& a = dprims[i];
+                const rtw_prim& b = dprims[i + 1];
+                const bool rect = a.type >= RTW_PRIM_RECT_XY && a.type <= RTW_PRIM_RECT_YZ;
+                if (!rect || b.type != a.type || a.p[4] == b.p[4]) continue;
+                bool same = true;
+                for (int k = 0; k < 4; ++k) same = same && a.p[k] == b.p[k];
+                if (!same) continue;
+                a.flip |= kRectPairHead;
+                ++i;  // b is the pair's second rect
+            }
+        }
+    }
     // ysphere_scan's fp32 prefilter records (rtw_device.h): spheres of
     // y-sphere runs whose centre (incl. motion) is within 2^8 and radius
     // within 2^4 are filtered, others (the random_balls ground, r = 1000)
