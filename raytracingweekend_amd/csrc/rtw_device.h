@@ -1094,10 +1094,22 @@ struct local_stack {
     int s[kStack];
     RTW_D int& at(int i) { return s[i]; }
 };
+// Workgroup size of the persistent BVH kernel (k_persist): its LDS node
+// packet is one per workgroup, so larger workgroups at the same waves per CU
+// share one larger packet.  1 024 threads = the CU's 16 waves in one
+// workgroup: one ~36 KB packet (1 152 nodes: all 969 of random_balls' tree)
+// instead of four ~8 KB copies (256 nodes each).  k_persist has no block
+// barrier in its loop, so the larger workgroup costs nothing else.
+// Measured (1 MI355X, A/B against 256, profiles/r03/ab_persist_block.log):
+// C3 slice 2 783 vs 2 607 Msamples/s (+6.7 %), C5 slice 623 vs 600 (+3.8 %).
+#ifndef RTW_PERSIST_BLOCK
+#define RTW_PERSIST_BLOCK 1024
+#endif
+constexpr int kPBlock = RTW_PERSIST_BLOCK;
 struct lds_stack {  // 16-bit node indices (LDS stacks need < 65536 nodes: upload)
     static constexpr int cap = kLdsStack;
-    uint16_t* p;  // &column[0][lane]; entry i at p[i * 256]
-    RTW_D uint16_t& at(int i) { return p[i * 256]; }
+    uint16_t* p;  // &column[0][lane]; entry i at p[i * kPBlock]
+    RTW_D uint16_t& at(int i) { return p[i * kPBlock]; }
     // a packet walk's wave-uniform stack: row 0 of the wave's 64 columns
     static constexpr int wave_cap = 64;
     RTW_D uint16_t* wave_row() const {

@@ -42,6 +42,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
+constexpr int kPWaves = kPBlock / 64;  // k_persist's workgroup (rtw_device.h kPBlock)
 
 // Path pool (SoA, one element per slot).  depth word of a slot:
 //   0                    empty
@@ -713,29 +714,29 @@ __device__ __forceinline__ const persist_args& args_now() {
 #define RTW_PERSIST_DIRECT(F) 0
 #endif
 template <int F, int M, bool LDS, bool LST = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
+__global__ __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist(persist_args) {
     constexpr bool DIRECT = RTW_PERSIST_DIRECT(F);
     constexpr bool BIN = RTW_BIN_RAYS(F) && !DIRECT;
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
-    __shared__ uint32_t s_cnt[kWaves];
-    __shared__ ray_batch s_batch[DIRECT ? 1 : kWaves];
-    __shared__ double s_ray[DIRECT ? 7 : 1][kBlock];  // DIRECT: each lane's ray (o, d, time)
-    __shared__ double s_thr[3][kBlock];  // each lane's path throughput
-    __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kBlock];
-    __shared__ uint32_t s_q[kBlock];     // each lane's sample id
+    __shared__ uint32_t s_cnt[kPWaves];
+    __shared__ ray_batch s_batch[DIRECT ? 1 : kPWaves];
+    __shared__ double s_ray[DIRECT ? 7 : 1][kPBlock];  // DIRECT: each lane's ray (o, d, time)
+    __shared__ double s_thr[3][kPBlock];  // each lane's path throughput
+    __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kPBlock];
+    __shared__ uint32_t s_q[kPBlock];     // each lane's sample id
     if (LDS) {
         const persist_args& A = args_now();
         const uint4* src = reinterpret_cast<const uint4*>(A.base);
         uint4* dst = reinterpret_cast<uint4*>(s_scene);
-        for (uint32_t k = threadIdx.x; k < A.bytes / 16; k += kBlock) dst[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < A.bytes / 16; k += kPBlock) dst[k] = src[k];
     }
     if (LST) {  // the BVH node packet (the top levels of every tree)
         const persist_args& A = args_now();
         const uint4* src = reinterpret_cast<const uint4*>(RTW_BVH4 ? (const void*)A.S.nodes4 : (const void*)A.S.nodes);
         uint4* dst = reinterpret_cast<uint4*>(s_scene + A.lds_nodes_off);
         constexpr uint32_t kNode16 = (uint32_t)((RTW_BVH4 ? sizeof(bvh_node4) : sizeof(bvh_node32)) / 16);
-        for (uint32_t k = threadIdx.x; k < A.lds_nodes * kNode16; k += kBlock) dst[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < A.lds_nodes * kNode16; k += kPBlock) dst[k] = src[k];
     }
     if (LDS || LST) __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
@@ -965,7 +966,7 @@ void k_persist(persist_args) {
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
-        for (int k = 0; k < kWaves; ++k) t += s_cnt[k];
+        for (int k = 0; k < kPWaves; ++k) t += s_cnt[k];
         if (t) atomicAdd(&args_now().C->segments[blockIdx.x % 8].v, t);
     }
 }
@@ -2545,8 +2546,11 @@ int blocks_per_cu(const void* fn, int block, size_t shm) {
         const auto it = cache.find(key);
         if (it != cache.end()) return it->second;
     }
+    // 0 when the block does not fit at all (too much LDS: node_packet probes
+    // sizes up to that point); 2 only when the query itself fails
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, block, shm) != hipSuccess || nb <= 0) return 2;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, block, shm) != hipSuccess) return 2;
+    nb = std::max(nb, 0);
     std::lock_guard<std::mutex> g(mu);
     cache[key] = nb;
     return nb;
@@ -2556,12 +2560,12 @@ int blocks_per_cu(const void* fn, int block, size_t shm) {
 // of blocks that can be resident at once, so every block starts immediately.
 template <int FF, int MM, bool LL, bool LST>
 int persist_grid(size_t shm, int cus) {
-    return blocks_per_cu(reinterpret_cast<const void*>(&k_persist<FF, MM, LL, LST>), kBlock, shm) * cus;
+    return std::max(1, blocks_per_cu(reinterpret_cast<const void*>(&k_persist<FF, MM, LL, LST>), kPBlock, shm)) * cus;
 }
 
 template <int FF, int MM, bool LL>
 int persist_sort_grid(size_t shm, int cus) {
-    return blocks_per_cu(reinterpret_cast<const void*>(&k_persist_sort<FF, MM, LL>), kSortBlock, shm) * cus;
+    return std::max(1, blocks_per_cu(reinterpret_cast<const void*>(&k_persist_sort<FF, MM, LL>), kSortBlock, shm)) * cus;
 }
 
 // The persistent kernels: material-regrouping k_persist_sort for list
@@ -2592,12 +2596,13 @@ uint32_t node_packet(size_t shm, int n_nodes) {
     cap = std::min<uint32_t>(cap, (uint32_t)std::max(0, n_nodes));
     if (!cap) return 0;
     const void* fn = reinterpret_cast<const void*>(&k_persist<FF, MM, LL, true>);
-    const int base = blocks_per_cu(fn, kBlock, shm);
+    const int base = blocks_per_cu(fn, kPBlock, shm);
+    if (base <= 0) return 0;
     const size_t off = (shm + 15) & ~size_t(15);
     uint32_t best = 0;
     for (uint32_t k = 32; k <= cap + 31; k += 32) {
         const uint32_t kk = std::min(k, cap);
-        if (blocks_per_cu(fn, kBlock, off + kk * kPacketNodeBytes) < base) break;
+        if (blocks_per_cu(fn, kPBlock, off + kk * kPacketNodeBytes) < base) break;
         best = kk;
         if (kk == cap) break;
     }
@@ -2620,18 +2625,22 @@ void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t s
     } else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack &&
                (RTW_BVH4 ? S.n_nodes4 > 0 : S.n_nodes < 65536)) {  // 16-bit LDS stacks
         if (name) *name = kname("k_persist", FF, MM, LL, true);
-        const uint32_t packet = node_packet<FF, MM, LL>(shm, RTW_BVH4 ? S.n_nodes4 : S.n_nodes);
+        uint32_t packet = node_packet<FF, MM, LL>(shm, RTW_BVH4 ? S.n_nodes4 : S.n_nodes);
         const uint32_t off = (uint32_t)((shm + 15) & ~size_t(15));
+        // a launch whose LDS does not fit would fault: no packet then
+        if (packet && blocks_per_cu(reinterpret_cast<const void*>(&k_persist<FF, MM, LL, true>), kPBlock,
+                                    off + packet * kPacketNodeBytes) <= 0)
+            packet = 0;
         g_node_packet = packet;
         const size_t shm2 = packet ? off + packet * kPacketNodeBytes : shm;
         if (!probe)
             hipLaunchKernelGGL((k_persist<FF, MM, LL, true>), dim3(persist_grid<FF, MM, LL, true>(shm, cus)),
-                               dim3(kBlock), shm2, st, persist_args{S, J, C, base, bytes, packet, off});
+                               dim3(kPBlock), shm2, st, persist_args{S, J, C, base, bytes, packet, off});
     } else {
         if (name) *name = kname("k_persist", FF, MM, LL, false);
         if (!probe)
             hipLaunchKernelGGL((k_persist<FF, MM, LL, false>), dim3(persist_grid<FF, MM, LL, false>(shm, cus)),
-                               dim3(kBlock), shm, st, persist_args{S, J, C, base, bytes});
+                               dim3(kPBlock), shm, st, persist_args{S, J, C, base, bytes});
     }
 }
 
@@ -2700,7 +2709,7 @@ template <int FF, bool LST>
 void launch_fast_t(bool probe, std::string* name, int cus, hipStream_t st, const fast_args& A) {
     if (name) *name = kname("k_fast", FF, -1, LST ? 1 : 0);
     if (probe) return;
-    const int grid = blocks_per_cu(reinterpret_cast<const void*>(&k_fast<FF, LST>), kBlock, 0) * cus;
+    const int grid = std::max(1, blocks_per_cu(reinterpret_cast<const void*>(&k_fast<FF, LST>), kBlock, 0)) * cus;
     hipLaunchKernelGGL((k_fast<FF, LST>), dim3(grid), dim3(kBlock), 0, st, A);
 }
 template <int FF, bool LL>
@@ -2709,7 +2718,7 @@ void launch_fast_sort_t(bool probe, std::string* name, int cus, hipStream_t st, 
     if (name) *name = kname("k_fast_sort", FF, -1, LL ? 1 : 0);
     if (probe) return;
     const size_t shm = LL ? bytes : 0;
-    const int grid = blocks_per_cu(reinterpret_cast<const void*>(&k_fast_sort<FF, LL>), kSortBlock, shm) * cus;
+    const int grid = std::max(1, blocks_per_cu(reinterpret_cast<const void*>(&k_fast_sort<FF, LL>), kSortBlock, shm)) * cus;
     hipLaunchKernelGGL((k_fast_sort<FF, LL>), dim3(grid), dim3(kSortBlock), shm, st, A, base, bytes);
 }
 // RTW_FAST_SORT=0: list scenes take k_fast too (A/B)
