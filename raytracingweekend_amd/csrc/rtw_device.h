@@ -950,8 +950,52 @@ RTW_D void rect_arbitrate(const scene& S, int pi, const ray& r, double t_min, hi
         h.rect = true;
     }
 }
+// A rect of plane axis K whose quotient t = (k - o.K) / d.K lies above h.t
+// is rejected by rect_axis_t's `t > t1` now and for every later (smaller)
+// h.t, so skipping it changes nothing.  That is certain without the division
+// when n = k - o.K (the test's own numerator) lies beyond
+// p2 = fl(fl(h.t d.K) (1 + 2^-50)) on d.K's side and |fl(h.t d.K)| > 2^-1000:
+// then |p2| >= |h.t d.K| (1 + 2^-51), so n / d.K > h.t (1 + 2^-51) >=
+// h.t + ulp(h.t) and the correctly rounded quotient is above h.t.  A zero or
+// NaN d.K, or an infinite product, is never skipped.
+template <int K, int A, int B>
+RTW_D void rect_arbitrate_far(const scene& S, int pi, const ray& r, double t_min, hit_state& h) {
+    const double ok = K == 0 ? r.o.x : (K == 1 ? r.o.y : r.o.z);
+    const double od = K == 0 ? r.d.x : (K == 1 ? r.d.y : r.d.z);
+    const double n = S.prims[pi].p[4] - ok;
+    const double p = h.t * od;
+    const double p2 = p * (1.0 + 0x1p-50);
+    const bool beyond = __builtin_fabs(p) > 0x1p-1000 && (od > 0 ? n > p2 : n < p2);
+    if (!beyond) rect_arbitrate<K, A, B>(S, pi, r, t_min, h);
+}
+// Box items test the face of each pair the ray can enter through first (the
+// lower plane when d.K > 0, of a box built with p0 <= p1; the pair's first
+// rect otherwise) and then the other three through rect_arbitrate_far: once
+// the ray has hit a near face, the far faces lie beyond it and cost no
+// division.  better() makes the winner independent of the test order
+// (its ties follow the list index, not the visiting order), and a skipped
+// rect could never have been accepted, so the result is box_arbitrate's in
+// list order exactly, whatever the box's orientation.  Measured (1 MI355X,
+// A/B, profiles/r03/ab_box_near_rejected.log): C5 slice 619.0 vs 621.9
+// Msamples/s (the C5 walk is bound by node-load latency and divergence, not
+// by the boxes' divisions; two more VGPR spills); GPU parity suite green with
+// it on.  Off; -DRTW_BOX_NEAR=1 selects it.
+#ifndef RTW_BOX_NEAR
+#define RTW_BOX_NEAR 0
+#endif
 template <bool U = false>
 RTW_D void box_arbitrate(const scene& S, int first, const ray& r, double t_min, hit_state& h) {
+    if constexpr (RTW_BOX_NEAR && !U) {
+        const int nz = first + (r.d.z > 0), ny = first + 2 + (r.d.y > 0), nx = first + 4 + (r.d.x > 0);
+        const int pair = 2 * first + 1;  // (first + 2j) + (first + 2j + 1) - 4j
+        rect_arbitrate<2, 0, 1>(S, nz, r, t_min, h);
+        rect_arbitrate<1, 0, 2>(S, ny, r, t_min, h);
+        rect_arbitrate<0, 1, 2>(S, nx, r, t_min, h);
+        rect_arbitrate_far<2, 0, 1>(S, pair - nz, r, t_min, h);
+        rect_arbitrate_far<1, 0, 2>(S, pair + 4 - ny, r, t_min, h);
+        rect_arbitrate_far<0, 1, 2>(S, pair + 8 - nx, r, t_min, h);
+        return;
+    }
     rect_arbitrate<2, 0, 1, U>(S, first, r, t_min, h);
     rect_arbitrate<2, 0, 1, U>(S, first + 1, r, t_min, h);
     rect_arbitrate<1, 0, 2, U>(S, first + 2, r, t_min, h);

@@ -650,9 +650,16 @@ __global__ __launch_bounds__(kBlock) RTW_SEG_ATTR void k_segment(scene S, job_t 
 // dry), every lane generates one ray into the wave's LDS buffer, and idle
 // lanes pop rays from that buffer.  A wave exits when the queue is exhausted,
 // its buffer is empty and its last path has ended.
-struct ray_batch {  // one wave's buffer of generated camera samples (LDS)
-    double ox[64], oy[64], oz[64], dx[64], dy[64], dz[64], tm[64];
-    uint32_t rng[64], q[64];
+// Camera samples a wave generates at once into its batch: 64 (lane-full
+// ray generation) unless RTW_PBATCH(F) says fewer for that kernel -- a
+// smaller batch leaves LDS for parked origins and the node packet.
+#ifndef RTW_PBATCH
+#define RTW_PBATCH(F) 64
+#endif
+template <int NB>
+struct ray_batch_t {  // one wave's buffer of generated camera samples (LDS)
+    double ox[NB], oy[NB], oz[NB], dx[NB], dy[NB], dz[NB], tm[NB];
+    uint32_t rng[NB], q[NB];
 };
 
 // Occupancy: left alone the compiler gives k_persist 160-230 VGPRs (2-3
@@ -713,15 +720,34 @@ __device__ __forceinline__ const persist_args& args_now() {
 #ifndef RTW_PERSIST_DIRECT
 #define RTW_PERSIST_DIRECT(F) 0
 #endif
+// PARK (RTW_PARK_ORIGIN): the batch-fed form with each lane's ray ORIGIN kept
+// in an LDS slot between iterations (written where the ray is taken or
+// continued, read before the walk and again before shading), so it is not a
+// register value live across the walk: what the media kernel spilled to
+// scratch was three doubles of the loop-carried ray.
+// Measured (1 MI355X, A/B, profiles/r03/ab_park_rejected.log): with the
+// 64-entry batch the parked origins take 24 KB from the node packet (C5 slice
+// 607.8 vs 623.3 Msamples/s); with 32-entry batches (RTW_PBATCH 32, half-lane
+// ray generation) the C5 kernel is spill-free (ScratchSize 0, 0 VGPR spills)
+// and its LDS 8 KB smaller, but measures 615.9 vs 623.3 (C5) and 2 609 vs
+// 2 783 (C3): the three spilled doubles (stored once per iteration, reloaded
+// at the shading sites) cost less than either.  Off.
+#ifndef RTW_PARK_ORIGIN
+#define RTW_PARK_ORIGIN(F) 0
+#endif
 template <int F, int M, bool LDS, bool LST = false>
 __global__ __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist(persist_args) {
     constexpr bool DIRECT = RTW_PERSIST_DIRECT(F);
     constexpr bool BIN = RTW_BIN_RAYS(F) && !DIRECT;
+    constexpr bool PARK = RTW_PARK_ORIGIN(F) && !DIRECT && !BIN;
+    constexpr int NB = DIRECT ? 1 : RTW_PBATCH(F);
+    static_assert(NB >= 1 && NB <= 64, "batch of one wave");
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kPWaves];
-    __shared__ ray_batch s_batch[DIRECT ? 1 : kPWaves];
-    __shared__ double s_ray[DIRECT ? 7 : 1][kPBlock];  // DIRECT: each lane's ray (o, d, time)
+    __shared__ ray_batch_t<NB> s_batch[DIRECT ? 1 : kPWaves];
+    // DIRECT: each lane's ray (o, d, time); PARK: its origin
+    __shared__ double s_ray[DIRECT ? 7 : (PARK ? 3 : 1)][kPBlock];
     __shared__ double s_thr[3][kPBlock];  // each lane's path throughput
     __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kPBlock];
     __shared__ uint32_t s_q[kPBlock];     // each lane's sample id
@@ -807,7 +833,7 @@ void k_persist(persist_args) {
         } else {
             // (the wave's batch too: formed once per kernel, its per-array
             // addresses were held in 15 VGPRs across the whole loop)
-            ray_batch& B = s_batch[tid >> 6];
+            ray_batch_t<NB>& B = s_batch[tid >> 6];
             for (int round = 0; round < 2; ++round) {
                 const unsigned long long m = __ballot(x.depth == 0);
                 if (!m) break;
@@ -816,8 +842,8 @@ void k_persist(persist_args) {
                     const persist_args& A = args_now();
                     const job_t& J = A.J;
                     ctrs_t* const C = A.C;
-                    // reserve up to 64 ids, own shard first
-                    uint32_t left = 64, given = 0, q = 0;
+                    // reserve up to NB ids, own shard first
+                    uint32_t left = NB, given = 0, q = 0;
                     bool got = false;
                     for (int a = 0; a < kQShards && left; ++a) {
                         const int sh = (own + a) % kQShards;
@@ -839,7 +865,7 @@ void k_persist(persist_args) {
                         left -= ok;
                     }
                     if (left) open = false;
-                    if (got) {
+                    if (got) {  // (lanes >= NB get no id)
                         uint32_t rng;
                         const ray r = camera_sample(J, q, rng);
                         B.ox[ln] = r.o.x, B.oy[ln] = r.o.y, B.oz[ln] = r.o.z;
@@ -858,6 +884,7 @@ void k_persist(persist_args) {
                 if (x.depth == 0 && rank < avail) {
                     const uint32_t k = bl + rank;
                     x.r = ray{d3{B.ox[k], B.oy[k], B.oz[k]}, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
+                    if constexpr (PARK) s_ray[0][tid] = x.r.o.x, s_ray[1][tid] = x.r.o.y, s_ray[2][tid] = x.r.o.z;
                     x.rng = B.rng[k];
                     const uint32_t hm = BIN ? home : tid;
                     s_q[hm] = B.q[k];
@@ -900,6 +927,7 @@ void k_persist(persist_args) {
         pf.mark(PS_LOAD);
         if (x.depth != 0) {
             if constexpr (DIRECT) x.r = unpark(tid);
+            if constexpr (PARK) x.r.o = d3{s_ray[0][tid], s_ray[1][tid], s_ray[2][tid]};
             const persist_args& A = args_now();
             scene S = A.S;
             hit_state h;
@@ -933,6 +961,10 @@ void k_persist(persist_args) {
                 asm volatile("" : "+v"(me)::"memory");
                 x.r = unpark(me);
             }
+            if constexpr (PARK) {
+                asm volatile("" : "+v"(me)::"memory");
+                x.r.o = d3{s_ray[0][me], s_ray[1][me], s_ray[2][me]};
+            }
             auto radiance = [&](const d3& L) {
                 double* o = A2.J.L + 3 * (size_t)s_q[me];
                 o[0] = L.x, o[1] = L.y, o[2] = L.z;
@@ -941,10 +973,12 @@ void k_persist(persist_args) {
             auto sk = make_sink(
                 [&](const d3& f, const ray& r) {
                     s_thr[0][me] *= f.x, s_thr[1][me] *= f.y, s_thr[2][me] *= f.z;
-                    if constexpr (DIRECT)
+                    if constexpr (DIRECT) {
                         park(me, r);  // the continuation waits in the lane's slot
-                    else
+                    } else {
                         nr = r;
+                        if constexpr (PARK) s_ray[0][me] = r.o.x, s_ray[1][me] = r.o.y, s_ray[2][me] = r.o.z;
+                    }
                 },
                 [&](const d3& E) { radiance(d3{s_thr[0][me], s_thr[1][me], s_thr[2][me]} * E); },
                 [&]() {
