@@ -112,6 +112,10 @@ struct fscene {
     float light_weight;
     float mv_t0, mv_inv_den;  // the common motion interval of the y-sphere runs' movers
     int32_t n_lights, world_bvh_root, render_type, background, n_media, n_runs, n_nodes;
+    // the BVH node packet in LDS (k_fast with LDS stacks: the top n_lnodes
+    // nodes of the BFS numbering, set by the kernel; 0 elsewhere)
+    const bvh_node32* lnodes;
+    int32_t n_lnodes;
 };
 
 // uniform (scalar) loads of a prim's fields
@@ -348,14 +352,42 @@ RTW_D bool slab(const bvh_node32& nd, const slab_rayf& s, float t0, float t1) {
                                      __builtin_fminf(__builtin_fmaxf(y0, y1), __builtin_fmaxf(z0, z1)));
     return tn <= tf * 1.00000024f;  // a 2-ulp allowance for the fp32 slab arithmetic
 }
-RTW_D bvh_node32 node_at(const fscene& S, int i) { return S.nodes[i]; }
+// (explicit address spaces, as rtwd::node_at: an LDS read for packet nodes,
+// a global read for the rest)
+RTW_D bvh_node32 node_at(const fscene& S, int i) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    using lds_v4 = const __attribute__((address_space(3))) v4u;
+    using glb_v4 = const __attribute__((address_space(1))) v4u;
+    v4u a, b;
+    if (i < S.n_lnodes) {
+        lds_v4* p = (lds_v4*)(S.lnodes + i);
+        a = p[0], b = p[1];
+    } else {
+        glb_v4* p = (glb_v4*)(S.nodes + i);
+        a = p[0], b = p[1];
+        asm volatile("" ::"v"(a.x));  // keeps the two loads apart (else they become one flat load)
+    }
+    bvh_node32 nd;
+    __builtin_memcpy(&nd, &a, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(&nd) + 16, &b, 16);
+    return nd;
+}
+
+// Workgroup size of k_fast: the LDS node packet is one per workgroup, so
+// larger workgroups at the same waves per CU share a larger packet (as
+// rtwd::kPBlock for k_persist); 1 024 threads = two workgroups of 16 waves
+// per CU at 8 waves per SIMD (rtw_kernels.hip RTW_FAST_BVH_WAVES: measured).
+#ifndef RTW_FAST_BLOCK
+#define RTW_FAST_BLOCK 1024
+#endif
+constexpr int kFastBlock = RTW_FAST_BLOCK;
 
 // traversal stacks: a column of 16-bit node ids per lane in LDS, or a
 // private array
 struct lds_stackf {
     static constexpr int cap = rtwd::kLdsStack;
     uint16_t* p;
-    RTW_D uint16_t& at(int i) { return p[i * 256]; }
+    RTW_D uint16_t& at(int i) { return p[i * kFastBlock]; }
 };
 struct priv_stackf {
     static constexpr int cap = rtwd::kStack;
@@ -727,7 +759,15 @@ RTW_D seg_f shade(const fscene& S, const fray& r, const fhit& h, uint32_t& rng, 
 }
 
 // the material class of a hit, the key the regrouping kernel sorts by
+// (the sorted block's order, as k_persist_sort's RTW_KEY_ORDER: material
+// order, path-ending keys last, unless RTW_KEY_ORDER selects another)
+#if defined(RTW_KEY_ORDER) && RTW_KEY_ORDER == 1
+enum { FK_LAMB = 0, FK_EMIT, FK_DIEL, FK_MISS, FK_METAL, FK_ISO, FK_IDLE, FK_N };
+#elif RTW_KEY_ORDER == 2
+enum { FK_LAMB = 0, FK_EMIT, FK_MISS, FK_DIEL, FK_METAL, FK_ISO, FK_IDLE, FK_N };
+#else
 enum { FK_LAMB = 0, FK_DIEL, FK_METAL, FK_ISO, FK_EMIT, FK_MISS, FK_IDLE, FK_N };
+#endif
 RTW_D int hit_key(const fscene& S, const fhit& h) {
     if (h.prim == -1) return FK_MISS;
     const int mat = h.prim <= -2 ? S.entries[-h.prim - 2].phase_material : S.prims[h.prim].material;

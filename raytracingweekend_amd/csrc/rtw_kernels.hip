@@ -1014,7 +1014,27 @@ void k_persist(persist_args) {
 // to the lane of their rank, so most waves run one branch.  Idle lanes end
 // up together at the top of the block: they take fresh camera samples
 // there, so ray generation also runs nearly lane-full.
+// The keys' order is the order of the sorted block.  A wave whose 64 slots
+// straddle two keys pays for both branches, which argues for the cheap keys
+// (emitter, miss: one radiance record) between the expensive ones
+// (RTW_KEY_ORDER 1: lambertian, emitter, dielectric, miss, ...; 2:
+// lambertian, emitter, miss, dielectric, ...).  Measured (1 MI355X, A/B,
+// profiles/r03/ab_key_order_rejected.log): T 3 961 (1) / 4 108 (2) vs 4 424
+// Msamples/s (0), T fp32 -8 %, C2 +0.6 %.  The paths that END (emitter,
+// miss) are the lanes that take camera samples next: in material order they
+// sit together at the block's top, beside the idle ones, and ray generation
+// runs lane-full in one or two waves; between the materials they are spread
+// over more waves.  0: material order, path-ending keys last.
+#ifndef RTW_KEY_ORDER
+#define RTW_KEY_ORDER 0
+#endif
+#if RTW_KEY_ORDER == 1
+enum { K_LAMB = 0, K_EMIT, K_DIEL, K_MISS, K_METAL, K_ISO, K_IDLE, K_N };
+#elif RTW_KEY_ORDER == 2
+enum { K_LAMB = 0, K_EMIT, K_MISS, K_DIEL, K_METAL, K_ISO, K_IDLE, K_N };
+#else
 enum { K_LAMB = 0, K_DIEL, K_METAL, K_ISO, K_EMIT, K_MISS, K_IDLE, K_N };
+#endif
 
 #ifndef RTW_SORT_BLOCK
 #define RTW_SORT_BLOCK 256
@@ -1245,6 +1265,7 @@ struct fast_args {
     job_t J;
     ctrs_t* C;
     rtwf::cam32 cam;
+    uint32_t lds_nodes;  // k_fast<.., LST>: BVH node packet (the top nodes) in dynamic LDS
 };
 
 // fast_args re-read from the kernarg segment by each phase that uses it
@@ -1256,15 +1277,31 @@ __device__ __forceinline__ const fast_args& fast_args_now() {
     return *(const fast_args*)p;
 }
 
+// Waves per SIMD of k_fast.  With the node packet, 8 waves in two
+// 1 024-thread workgroups per CU (each with a ~48 KB packet) beat 6 waves in
+// two 768-thread ones (~56 KB packets, no spills) although the kernel then
+// spills ~17 VGPRs: C3 fp32 4 710 vs 4 386, C5 fp32 806 vs 728 Msamples/s;
+// one 1 024-thread workgroup at 6 waves (16 waves per CU) 3 350 / 536; 384
+// threads at 6 waves 3 602 / 556; no packet at 6 waves (round 3 before it)
+// 3 553 / 645 (1 MI355X, A/B, profiles/r03/ab_fp32_packet.log).
 #ifndef RTW_FAST_BVH_WAVES
-#define RTW_FAST_BVH_WAVES 6
+#define RTW_FAST_BVH_WAVES 8
 #endif
 template <int F, bool LST>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RTW_FAST_BVH_WAVES)))
+__global__ __launch_bounds__(rtwf::kFastBlock) __attribute__((amdgpu_waves_per_eu(RTW_FAST_BVH_WAVES)))
 void k_fast(fast_args) {
     using namespace rtwf;
-    __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kBlock];
-    __shared__ uint32_t s_cnt[kWaves];
+    constexpr int kFW = kFastBlock / 64;
+    extern __shared__ __attribute__((aligned(16))) char s_nodes[];
+    __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kFastBlock];
+    __shared__ uint32_t s_cnt[kFW];
+    if (LST) {  // the BVH node packet (the top levels of every tree)
+        const fast_args& A = fast_args_now();
+        const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
+        uint4* dst = reinterpret_cast<uint4*>(s_nodes);
+        for (uint32_t k = threadIdx.x; k < A.lds_nodes * 2; k += kFastBlock) dst[k] = src[k];
+        __syncthreads();
+    }
     const uint32_t lane = threadIdx.x & 63;
     const int own = blockIdx.x % kQShards;
     fray r{f3{0, 0, 0}, f3{0, 0, 1}, 0};
@@ -1318,7 +1355,11 @@ void k_fast(fast_args) {
         fhit h;
         if constexpr (LST) {
             lds_stackf stk{&s_stack[0][threadIdx.x]};
-            h = world_closest<F>(fast_args_now().S, r, rng, stk);
+            const fast_args& A = fast_args_now();
+            fscene S = A.S;
+            S.lnodes = reinterpret_cast<const bvh_node32*>(s_nodes);
+            S.n_lnodes = (int32_t)A.lds_nodes;
+            h = world_closest<F>(S, r, rng, stk);
         } else {
             priv_stackf stk;
             h = world_closest<F>(fast_args_now().S, r, rng, stk);
@@ -1346,7 +1387,7 @@ void k_fast(fast_args) {
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
-        for (int k = 0; k < kWaves; ++k) t += s_cnt[k];
+        for (int k = 0; k < kFW; ++k) t += s_cnt[k];
         if (t) atomicAdd(&fast_args_now().C->segments[blockIdx.x % 8].v, t);
     }
 }
@@ -2736,6 +2777,26 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
     return false;
 }
 
+// BVH node packet of a k_fast<.., LST> launch: the most top nodes that fit
+// in LDS beside the stacks without costing a workgroup per CU (node_packet's
+// rule; RTW_LDS_NODES caps it, 0 = off).
+uint32_t fast_node_packet(const void* fn, int n_nodes) {
+    const char* e = std::getenv("RTW_LDS_NODES");
+    uint32_t cap = (e && *e) ? (uint32_t)std::max(0, std::atoi(e)) : 4096u;
+    cap = std::min<uint32_t>(cap, (uint32_t)std::max(0, n_nodes));
+    if (!cap) return 0;
+    const int base = blocks_per_cu(fn, rtwf::kFastBlock, 0);
+    if (base <= 0) return 0;
+    uint32_t best = 0;
+    for (uint32_t k = 32; k <= cap + 31; k += 32) {
+        const uint32_t kk = std::min(k, cap);
+        if (blocks_per_cu(fn, rtwf::kFastBlock, kk * sizeof(bvh_node32)) < base) break;
+        best = kk;
+        if (kk == cap) break;
+    }
+    return best;
+}
+
 // The fp32 fast-mode kernel of a scene: one instantiation per traversal
 // feature set, LDS stacks when the deepest walk fits them.  grid = resident
 // blocks (occupancy query, cached).  probe: name it only.
@@ -2743,8 +2804,12 @@ template <int FF, bool LST>
 void launch_fast_t(bool probe, std::string* name, int cus, hipStream_t st, const fast_args& A) {
     if (name) *name = kname("k_fast", FF, -1, LST ? 1 : 0);
     if (probe) return;
-    const int grid = std::max(1, blocks_per_cu(reinterpret_cast<const void*>(&k_fast<FF, LST>), kBlock, 0)) * cus;
-    hipLaunchKernelGGL((k_fast<FF, LST>), dim3(grid), dim3(kBlock), 0, st, A);
+    const void* fn = reinterpret_cast<const void*>(&k_fast<FF, LST>);
+    fast_args a = A;
+    a.lds_nodes = LST ? fast_node_packet(fn, A.S.n_nodes) : 0u;
+    const size_t shm = (size_t)a.lds_nodes * sizeof(bvh_node32);
+    const int grid = std::max(1, blocks_per_cu(fn, rtwf::kFastBlock, shm)) * cus;
+    hipLaunchKernelGGL((k_fast<FF, LST>), dim3(grid), dim3(rtwf::kFastBlock), shm, st, a);
 }
 template <int FF, bool LL>
 void launch_fast_sort_t(bool probe, std::string* name, int cus, hipStream_t st, const fast_args& A,
