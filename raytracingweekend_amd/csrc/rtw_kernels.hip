@@ -1420,7 +1420,7 @@ __device__ __forceinline__ rtwf::fscene lds_fscene(const rtwf::fscene& S, const 
 // slot; throughputs stay in home slots.  LDS: the fp32 scene (when it fits)
 // for shading, traversal reads the scene through the scalar cache.
 #ifndef RTW_FAST_WAVES
-#define RTW_FAST_WAVES 6  // T fp32: 6 465 (5 waves), 5 601 (4), 7 000 (6)
+#define RTW_FAST_WAVES 7  // T fp32: 5 601 (4 waves), 6 465 (5), 7 000 (6), 7 136 (7), 6 462 (8): profiles/r03/ab_fp32_sort_waves.log, ab_fp32_sort_waves7.log
 #endif
 template <int F, bool LDS>
 __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(RTW_FAST_WAVES)))
