@@ -104,3 +104,39 @@ def test_fast_mode_shards_and_passes(gpu, monkeypatch):
     assert np.allclose(parts, whole, rtol=1e-12, atol=1e-12)
     assert st3["launches_intersect"] == 3 and np.array_equal(passes, whole)
     assert st3["segments"] == st["segments"]
+
+
+def _render_child(env, scene, nx, ny, spp, depth, seed, bvh, precision):
+    """Render in a fresh process with extra environment (RTW_LDS_NODES is
+    read per launch, but a child keeps the switch away from this process)."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / "acc.npy"
+        code = (f"import sys; sys.path.insert(0, {str(root)!r}); import numpy as np; "
+                f"from raytracingweekend_amd import render as r; "
+                f"ds = r.DeviceScene(r.SceneDesc({scene!r}, {nx}/{ny}, use_bvh={bvh})); "
+                f"a, st = ds.render_accumulate({nx}, {ny}, {spp}, {depth}, seed={seed}, precision={precision!r}); "
+                f"ds.close(); np.save({str(out)!r}, a); print('SEGMENTS', st['segments'])")
+        r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env}, check=True, timeout=300,
+                           capture_output=True, text=True)
+        segs = int(r.stdout.split("SEGMENTS")[-1].split()[0])
+        return np.load(out), segs
+
+
+@pytest.mark.parametrize("scene", ["random_balls", "book2_final"])
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_node_packet_changes_no_sample(gpu, scene, precision):
+    """The BVH node packet (the top nodes staged in LDS: k_persist for fp64,
+    k_fast for fp32) only changes where a node is read from: the render with
+    it equals the render without it (RTW_LDS_NODES=0) bit for bit, with the
+    same traversal count."""
+    nx, ny, spp, depth = 96, 64, 4, 50
+    with_p, s1 = _render_child({}, scene, nx, ny, spp, depth, 7, True, precision)
+    without, s0 = _render_child({"RTW_LDS_NODES": "0"}, scene, nx, ny, spp, depth, 7, True, precision)
+    assert s1 == s0 and np.array_equal(with_p, without)
+    assert np.all(np.isfinite(with_p)) and with_p.sum() > 0
