@@ -1252,6 +1252,19 @@ RTW_D void push_children(const bvh_node32& nd, int dneg, STK& stk, int& sp) {
 #ifndef RTW_CHILD_TEST
 #define RTW_CHILD_TEST 1
 #endif
+// Speculative while-while for the world child-test walk (Aila & Laine 2009):
+// lanes that already hold their leaf keep walking until every lane of the
+// wave has one, so the inner loop runs with more lanes busy.  Nodes are then
+// sometimes tested against a closest t the pending leaf would have
+// tightened: more work per lane, never a different winner (better() makes
+// it order-independent).
+#ifndef RTW_SPEC_WALK
+#define RTW_SPEC_WALK 1
+#endif
+// ... and for the group BVH walks (while-while form)
+#ifndef RTW_SPEC_GROUP
+#define RTW_SPEC_GROUP 0
+#endif
 
 RTW_D double widen_lo(double t) { return t > 0 ? t * 0.5 : t * 2.0 - 1e-9; }
 RTW_D double widen_hi(double t) { return t * (1 + 1e-12) + 1e-9; }
@@ -1461,6 +1474,33 @@ RTW_D void group_bvh(const scene& S, int root, int root4, const ray& r, double t
     // while-while, as in world_closest (+6.6 % Book 2 BVH, whose 1 000-sphere
     // cluster is a group BVH).  (The world walk's child-test form measured
     // -0.4 % here, C5.)
+#if RTW_SPEC_GROUP
+    // speculative (RTW_SPEC_WALK's reasoning): a lane holding its leaf keeps
+    // popping nodes while other lanes look for theirs; a second leaf it meets
+    // goes back on its stack for the next round
+    for (;;) {
+        int la = 0, lc = 0;
+        bool stall = false;  // met its second leaf: waits for the others
+        for (;;) {
+            if (__builtin_amdgcn_ballot_w64(lc == 0 && sp > base) == 0) break;
+            if (sp == base || stall) continue;
+            const int ni = stk.at(--sp);
+            const bvh_node32 nd = node_at(S, ni);
+            if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
+            const int c = node_count(nd);
+            if (c == 0) {
+                if (sp + 2 <= STK::cap) push_children(nd, dneg, stk, sp);
+            } else if (lc == 0) {
+                la = nd.a, lc = c;
+            } else {
+                stk.at(sp++) = ni;  // tested again when popped
+                stall = true;
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(lc != 0) == 0) break;
+        for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
+    }
+#else
     for (;;) {
         int la = 0, lc = 0;
         while (lc == 0 && sp > base) {
@@ -1473,6 +1513,7 @@ RTW_D void group_bvh(const scene& S, int root, int root4, const ray& r, double t
         if (lc == 0) break;
         for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
     }
+#endif
 #else
     stk.at(sp++) = root;
     while (sp > base) {
@@ -1618,6 +1659,29 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             sp = 0;
             for (;;) {
                 int la = 0, lc = 0;  // this lane's pending leaf: first item, count
+#if RTW_SPEC_WALK
+                // speculative while-while: a lane that holds its leaf keeps
+                // walking (with the closest t it has) while other lanes of the
+                // wave still look for theirs, and stops at its next leaf,
+                // which it keeps as its current node for the next round
+                for (;;) {
+                    const bool done = !have && sp == 0;
+                    if (__builtin_amdgcn_ballot_w64(lc == 0 && !done) == 0) break;
+                    if (done || (have && cb < 0 && lc != 0)) continue;
+                    if (!have) {
+                        const bvh_node32 nd = node_at(S, stk.at(--sp));
+                        if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
+                        ca = nd.a, cb = nd.b, have = true;
+                    }
+                    if (cb < 0) {  // a leaf
+                        if (lc == 0) la = ca, lc = -cb, have = false;
+                        continue;
+                    }
+                    have = expand_children(S, sr, t0, t_hi32(h.t), dneg, stk, sp, ca, cb);
+                }
+                if (__builtin_amdgcn_ballot_w64(lc != 0) == 0) break;
+                if (lc != 0) leaf(la, lc);
+#else
                 while (lc == 0) {
                     if (!have) {
                         if (sp == 0) break;
@@ -1633,6 +1697,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                 }
                 if (lc == 0) break;
                 leaf(la, lc);
+#endif
             }
         } else if constexpr ((F & F_GBVH) == 0) {
             // while-while: each lane walks inner nodes until it reaches a

@@ -373,6 +373,9 @@ RTW_D bvh_node32 node_at(const fscene& S, int i) {
     return nd;
 }
 
+#ifndef RTW_FAST_SPEC
+#define RTW_FAST_SPEC 0
+#endif
 // Workgroup size of k_fast: the LDS node packet is one per workgroup, so
 // larger workgroups at the same waves per CU share a larger packet (as
 // rtwd::kPBlock for k_persist); 1 024 threads = two workgroups of 16 waves
@@ -458,6 +461,46 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
         const float t0 = kTMinF * 0.5f;
         int sp = 0;
         stk.at(sp++) = S.world_bvh_root;
+#if RTW_FAST_SPEC
+        // speculative while-while (rtwd::RTW_SPEC_WALK): lanes walk inner
+        // nodes until every lane holds a leaf or is out of nodes; a lane that
+        // meets a second leaf puts it back and waits; then the leaves are
+        // tested together
+        for (;;) {
+            int la = 0, lc = 0;
+            bool stall = false;
+            for (;;) {
+                if (__builtin_amdgcn_ballot_w64(lc == 0 && sp > 0) == 0) break;
+                if (sp == 0 || stall) continue;
+                const int ni = stk.at(--sp);
+                const bvh_node32 nd = node_at(S, ni);
+                if (!slab(nd, sr, t0, h.t)) continue;
+                if (nd.b >= 0) {
+                    if (sp + 2 <= STK::cap) stk.at(sp++) = nd.b & 0x0fffffff, stk.at(sp++) = nd.a;
+                } else if (lc == 0) {
+                    la = nd.a, lc = -nd.b;
+                } else {
+                    stk.at(sp++) = ni;  // tested again when popped
+                    stall = true;
+                }
+            }
+            if (__builtin_amdgcn_ballot_w64(lc != 0) == 0) break;
+            for (int k = 0; k < lc; ++k) {
+                const int it = S.items[la + k];
+                if (it < 0) {  // a plain one-prim entry: ~prim
+                    arbitrate(S, ~it, r, kTMinF, h);
+                    continue;
+                }
+                const ent_v e = view_entry<false>(S, it);
+                const fray lr = ops_in<false>(e, r, 0, e.n_ops);
+                if ((F & rtwd::F_GBVH) && e.bvh_root >= 0)
+                    group_bvh(S, e.bvh_root, lr, kTMinF, h, stk, sp);
+                else
+                    for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMinF, h);
+            }
+        }
+        if (false)
+#endif
         while (sp > 0) {
             const bvh_node32 nd = node_at(S, stk.at(--sp));
             if (!slab(nd, sr, t0, h.t)) continue;
