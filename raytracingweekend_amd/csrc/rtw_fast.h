@@ -373,6 +373,10 @@ RTW_D bvh_node32 node_at(const fscene& S, int i) {
     return nd;
 }
 
+// Speculative while-while for the fp32 world walk (RTW_SPEC_WALK's form
+// without the child test): measured C3 fp32 4 142 vs 4 703 Msamples/s (1
+// MI355X, A/B, profiles/r03/ab_fp32_spec_rejected.log; the 8-wave kernel
+// spills more around the two-level loop).  Off.
 #ifndef RTW_FAST_SPEC
 #define RTW_FAST_SPEC 0
 #endif
