@@ -46,10 +46,27 @@ sys.path.insert(0, str(ROOT))
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"] if (ROOT / "BASELINE.json").exists() else \
     "Msamples/s (rays traced/s) at fixed W×H×spp×max_depth; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# fp64 VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction
-VALU_PEAK_GINST = 1024 * 2.4 / 4
-# VALU issue cycles available: 1024 SIMDs x 2.4 GHz
+# VALU issue cycles available: 256 CUs x 4 SIMDs x 2.4 GHz
 VALU_SIMD_GCYC = 1024 * 2.4
+# fp64 vector peak: 1024 SIMDs x 2.4 GHz x 32 FLOP/cycle (16 fp64 FMA lanes)
+FP64_PEAK_TFLOPS = 78.6
+FP32_PEAK_TFLOPS = 157.3
+# Issue cost of one wave64 VALU instruction per SIMD, in cycles at the nominal
+# 2.4 GHz, per SQ_INSTS_VALU_* class: measured on the card with independent
+# chains at 4 waves/SIMD (scripts/valu_rates.hip; profiles/r01/valu_rates.log,
+# profiles/r04/valu_rates.log).  Each class takes its cheapest measured
+# member (F64: fma/mul/add 4.6, div_scale / fixup 4.6-4.8; TRANS_F64:
+# rcp/rsq 16.6-16.8; INT32: v_add_u32 2.55, v_mul_lo_u32 4.35; INT64:
+# v_mad_u64_u32 5.15; CVT: v_cvt_f64_u32 5.26, v_cvt_f32_f64 5.33; F32:
+# v_add_f32 2.60, v_fma_f32 2.70; TRANS_F32: v_rcp/v_sqrt/v_exp/v_log/v_sin
+# _f32), and instructions no class counts (moves, compares, selects, logic)
+# take the cheapest rate of all -- so the class-weighted cycles are a LOWER
+# bound of the SIMD's VALU issue time and their fraction of the SIMD cycles
+# is at most 1 when the rates hold.
+VALU_COST = {"FMA_F64": 4.59, "MUL_F64": 4.59, "ADD_F64": 4.59, "TRANS_F64": 16.6,
+             "INT32": 2.55, "INT64": 5.15, "CVT": 5.26,
+             "FMA_F32": 2.60, "ADD_F32": 2.60, "MUL_F32": 2.60, "TRANS_F32": 4.4}
+VALU_COST_OTHER = 2.55
 PMC_DIR = ROOT / "profiles" / "pmc"
 
 # BASELINE.json configs; spp is the image's TOTAL samples per pixel
@@ -185,52 +202,74 @@ def spawn(args) -> int:
 
 
 def roofline(args, kernel, build, seg, ms, launches, algo):
-    """Roofline object of the traversal kernel (per launch averages)."""
+    """Roofline object of the traversal kernel (per launch averages).
+
+    The headline (bound / achieved / peak / frac) is SURVEY.md 8(d)'s HBM
+    figure: 68 algorithmic bytes per traversal (36 in fp32) x device-counted
+    traversals / HIP-event launch time, against 8 TB/s; `traffic` = the HBM
+    bytes the PMC record of this kernel, build and workload measured.  Beside
+    it, `valu` (from the same record): (i) class-weighted VALU issue cycles
+    over the SIMDs' cycles, (ii) the fp64 FLOP rate against the vector peak,
+    and the lane utilisation.  Every fraction is bounded by 1 (checked)."""
     avg_ms = ms / max(launches, 1)
     seg_launch = seg / max(launches, 1)
     hbm_ach = algo / (ms * 1e-3) / 1e9
-    hbm = {"achieved": round(hbm_ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(hbm_ach / HBM_PEAK_GBS, 4), "bytes_per_segment": round(algo / max(seg, 1), 2),
+    out = {"kernel": kernel, "build_id": build, "launches": int(launches), "avg_launch_ms": round(avg_ms, 4),
+           "segments_per_launch": round(seg_launch, 1),
+           "bound": "hbm", "achieved": round(hbm_ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(hbm_ach / HBM_PEAK_GBS, 4), "traffic": None,
+           "bytes_per_segment": round(algo / max(seg, 1), 2),
            "algo_bytes_per_launch": round(algo / max(launches, 1), 1),
            "definition": "SURVEY.md 8(d): 68 algorithmic bytes per traversal in fp64 (ray 56 B in, hit 12 B out; "
-                         "36 B in the fp32 fast mode) x device-counted traversals / HIP-event launch time"}
+                         "36 B in the fp32 fast mode) x device-counted traversals / HIP-event launch time, against "
+                         "8 TB/s; traffic = PMC FETCH_SIZE + WRITE_SIZE bytes per launch of the same kernel and build"}
     rec, src = find_pmc(kernel, build, pmc_key(args))
-    out = {"kernel": kernel, "build_id": build, "launches": int(launches), "avg_launch_ms": round(avg_ms, 4),
-           "segments_per_launch": round(seg_launch, 1)}
+    out["pmc"] = src
     if rec is None:
-        out.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": hbm["frac"], "traffic": None, "pmc": src, "hbm": hbm})
         return out
     scale = seg_launch / rec["segments_per_launch"]  # PMC bytes per launch, scaled by traversals
-    traffic = round(rec["hbm_bytes_per_launch"] * scale, 1)
-    hbm["traffic"] = traffic
-    ipw = rec["valu_insts_per_wave_segment"]
-    issue = ipw * seg_launch / 64 / (avg_ms * 1e-3) / 1e9
-    out.update({"traffic": traffic, "valu_insts_per_wave_segment": round(ipw, 1), "pmc": src, "hbm": hbm,
-                "issue_model": {"achieved": round(issue, 1), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
-                                "frac": round(issue / VALU_PEAK_GINST, 4),
-                                "definition": "VALU wave-instructions (SQ_INSTS_VALU) x traversals / launch time, "
-                                              "every instruction priced at the fp64 rate (4 cycles per SIMD)"}})
-    busy = rec.get("valu_busy_cycles_per_segment")
-    if busy:
-        # measured: the cycles the SIMDs spent issuing VALU instructions
-        # (4 x SQ_ACTIVE_INST_VALU per traversal of the record) x this run's
-        # traversals / its HIP-event launch time, against every SIMD busy
-        ach = busy * seg_launch / (avg_ms * 1e-3) / 1e9
-        lane = rec.get("valu_lane_util")
-        out.update({"bound": "valu", "achieved": round(ach, 1), "peak": VALU_SIMD_GCYC, "unit": "G SIMD-cycles/s",
-                    "frac": round(ach / VALU_SIMD_GCYC, 4),
-                    "valu_lane_util": round(lane, 4) if lane else None,
-                    "valu_useful_frac": round(ach / VALU_SIMD_GCYC * lane, 4) if lane else None,
-                    "definition": "VALU-busy SIMD cycles per traversal (4 x SQ_ACTIVE_INST_VALU of the PMC record of "
-                                  "this kernel, build and workload) x device-counted traversals / HIP-event launch "
-                                  "time, against 1024 SIMDs x 2.4 GHz; valu_lane_util = SQ_THREAD_CYCLES_VALU / (64 x "
-                                  "SQ_ACTIVE_INST_VALU), the share of lanes doing work in those cycles"})
-    else:
-        out.update({"bound": "valu", "achieved": round(issue, 1), "peak": VALU_PEAK_GINST,
-                    "unit": "G wave-instr/s", "frac": round(issue / VALU_PEAK_GINST, 4),
-                    "definition": out["issue_model"]["definition"]})
+    out["traffic"] = round(rec["hbm_bytes_per_launch"] * scale, 1)
+    if rec.get("write_bytes_per_launch") is not None:
+        out["write_bytes"] = round(rec["write_bytes_per_launch"] * scale, 1)
+    secs = avg_ms * 1e-3
+    v = {"valu_insts_per_wave_segment": round(rec["valu_insts_per_wave_segment"], 1),
+         "lane_util": round(rec["valu_lane_util"], 4) if rec.get("valu_lane_util") else None}
+    cyc = rec.get("valu_class_cycles_per_segment")
+    if cyc:
+        ach = cyc * seg_launch / secs / 1e9
+        v["class_weighted"] = {
+            "achieved": round(ach, 1), "peak": VALU_SIMD_GCYC, "unit": "G SIMD-cycles/s",
+            "frac": round(ach / VALU_SIMD_GCYC, 4), "cycles_per_segment": round(cyc, 2),
+            "definition": "SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64, _INT32, _INT64, _CVT, _{FMA,ADD,MUL,TRANS}_F32 "
+                          "x their measured issue cycles (VALU_COST), unclassified VALU at the cheapest rate, per "
+                          "traversal of the PMC record x this run's traversals / launch time, against 1024 SIMDs "
+                          "x 2.4 GHz (a lower bound of VALU issue time)"}
+        if v["lane_util"]:
+            v["useful_frac"] = round(ach / VALU_SIMD_GCYC * v["lane_util"], 4)
+    fl = rec.get("fp64_flops_per_segment")
+    if fl is not None:
+        tf = fl * seg_launch / secs / 1e12
+        v["fp64_flops"] = {"achieved": round(tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(tf / FP64_PEAK_TFLOPS, 4),
+                           "definition": "SQ_INSTS_VALU_FLOPS_FP64 (+ _TRANS) per traversal x traversals / launch "
+                                         "time, against the 78.6 TF fp64 vector peak"}
+    fl32 = rec.get("fp32_flops_per_segment")
+    if fl32:
+        tf = fl32 * seg_launch / secs / 1e12
+        v["fp32_flops"] = {"achieved": round(tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(tf / FP32_PEAK_TFLOPS, 4)}
+    out["valu"] = v
+    check_fracs(out)
     return out
+
+
+def check_fracs(obj, path="roofline"):
+    """Every `frac` of a roofline object is a fraction of a peak: in [0, 1]."""
+    if isinstance(obj, dict):
+        for k, val in obj.items():
+            if k == "frac" and not (0.0 <= val <= 1.0):
+                raise ValueError(f"{path}.frac = {val} is not a roofline fraction")
+            check_fracs(val, f"{path}.{k}")
 
 
 def main():

@@ -242,12 +242,20 @@ typedef struct rtw_render_params {
     int32_t spp_count;     /* (sample-range sharding; 0 = all of [spp_begin, spp))  */
     int32_t row_begin;     /* ... of rows j = row_begin + k*row_step (pixel sharding) */
     int32_t row_step;      /* 0 or 1 = every row                                    */
-    int32_t accum_on_device; /* 1: accum_rgb is a device pointer on this handle's GPU */
+    int32_t accum_on_device; /* 1: accum_rgb is device memory of this handle's GPU
+                                (hipMalloc / torch allocators) or managed memory
+                                (hipMallocManaged); anything else: RTW_ERR_INVALID */
     int32_t collect_kernel_times; /* 1: hipEvents around traversal launches,    */
                                   /* 2: and shade launches (adds queue gaps)   */
     int32_t wavefront_paths; /* paths in flight (0 = library default)             */
-    int32_t precision;     /* rtw_precision: RTW_PRECISION_FP64 (0) = the reference's
-                              double arithmetic, parity with the CPU renderer;
+    int32_t precision;     /* rtw_precision: RTW_PRECISION_FP64 (0) = parity with the
+                              CPU renderer: every path decision (rays, hit
+                              distances, comparisons, random draws) in the
+                              reference's IEEE double arithmetic; the radiance-only
+                              factors (lambertian weight, pdf quotients) with fewer
+                              divisions, a few ulps off (build with
+                              -DRTW_RADIANCE_FAST=0 for the reference's own
+                              expressions there too);
                               RTW_PRECISION_FP32 (1) = fast mode, single precision
                               traversal and shading, statistical parity only     */
 } rtw_render_params;

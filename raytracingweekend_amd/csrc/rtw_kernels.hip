@@ -1039,6 +1039,18 @@ enum { K_LAMB = 0, K_DIEL, K_METAL, K_ISO, K_EMIT, K_MISS, K_IDLE, K_N };
 #ifndef RTW_SORT_BLOCK
 #define RTW_SORT_BLOCK 256
 #endif
+// Ray generation threshold: a wave takes camera samples only when at least
+// this many of its lanes are idle.  After shading a few lambertian paths per
+// wave end (pdf <= 0, depth), and a wave would run a whole camera_sample
+// (~150 VALU) for one to three lanes; with fewer than K idle lanes the slots
+// wait one iteration, are sorted to the block's top with the other idle
+// records (K_IDLE) and refill there, lane-full.  A block always ends with
+// every wave fully idle, so the queue still drains.  Measured (1 MI355X,
+// A/B, profiles/r03/ab_refill_min.log): K = 8 T +0.45 %, C2 +0.8 %; K = 24
+// T +0.2 %, C2 -0.7 %.
+#ifndef RTW_REFILL_MIN
+#define RTW_REFILL_MIN 8
+#endif
 constexpr int kSortBlock = RTW_SORT_BLOCK;  // paths regrouped together (one workgroup)
 constexpr int kSortWaves = kSortBlock / 64;
 template <int F, int M, bool LDS>
@@ -1083,7 +1095,7 @@ void k_persist_sort(persist_args) {
         {
             const bool idle = x.depth == 0;
             const unsigned long long m = __ballot(idle);
-            if (open && m) {
+            if (open && __popcll(m) >= RTW_REFILL_MIN) {
                 const persist_args& A = args_now();
                 const job_t& J = A.J;
                 ctrs_t* const C = A.C;
@@ -2608,39 +2620,47 @@ bool launch_segment(bool probe, int f, int mask, int grid, hipStream_t st, const
 // Resident workgroups per CU of kernel `fn` at `block` threads and `shm`
 // bytes of dynamic LDS on the current device: one occupancy query per
 // (kernel, block, LDS bytes, device), cached.  rtw_render_multi renders from
-// one host thread per device at once, so the cache is guarded; a failed
-// query is not cached (2 blocks per CU is assumed for that launch).
+// one host thread per device at once, so the cache is guarded.  Returns 0
+// when the block does not fit at all and -1 when the query itself fails (not
+// cached): the packet probes and the LDS guard read -1 as "does not fit", only
+// grid sizing (grid_blocks) falls back to 2 workgroups per CU.
 int blocks_per_cu(const void* fn, int block, size_t shm) {
     static std::mutex mu;
     static std::map<std::tuple<const void*, int, size_t, int>, int> cache;
     int dev = -1;
-    if (hipGetDevice(&dev) != hipSuccess) return 2;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
     const auto key = std::make_tuple(fn, block, shm, dev);
     {
         std::lock_guard<std::mutex> g(mu);
         const auto it = cache.find(key);
         if (it != cache.end()) return it->second;
     }
-    // 0 when the block does not fit at all (too much LDS: node_packet probes
-    // sizes up to that point); 2 only when the query itself fails
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, block, shm) != hipSuccess) return 2;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, block, shm) != hipSuccess) return -1;
     nb = std::max(nb, 0);
     std::lock_guard<std::mutex> g(mu);
     cache[key] = nb;
     return nb;
 }
 
+// Grid of a persistent launch: resident workgroups per CU x CUs; a failed
+// occupancy query assumes 2 per CU, a block that does not fit still gets 1
+// per CU (the LDS guards in the launchers refuse those before this).
+int grid_blocks(const void* fn, int block, size_t shm, int cus) {
+    const int nb = blocks_per_cu(fn, block, shm);
+    return (nb < 0 ? 2 : std::max(1, nb)) * cus;
+}
+
 // Persistent kernel for the same instantiation set.  The grid is the number
 // of blocks that can be resident at once, so every block starts immediately.
 template <int FF, int MM, bool LL, bool LST>
 int persist_grid(size_t shm, int cus) {
-    return std::max(1, blocks_per_cu(reinterpret_cast<const void*>(&k_persist<FF, MM, LL, LST>), kPBlock, shm)) * cus;
+    return grid_blocks(reinterpret_cast<const void*>(&k_persist<FF, MM, LL, LST>), kPBlock, shm, cus);
 }
 
 template <int FF, int MM, bool LL>
 int persist_sort_grid(size_t shm, int cus) {
-    return std::max(1, blocks_per_cu(reinterpret_cast<const void*>(&k_persist_sort<FF, MM, LL>), kSortBlock, shm)) * cus;
+    return grid_blocks(reinterpret_cast<const void*>(&k_persist_sort<FF, MM, LL>), kSortBlock, shm, cus);
 }
 
 // The persistent kernels: material-regrouping k_persist_sort for list
@@ -2808,7 +2828,7 @@ void launch_fast_t(bool probe, std::string* name, int cus, hipStream_t st, const
     fast_args a = A;
     a.lds_nodes = LST ? fast_node_packet(fn, A.S.n_nodes) : 0u;
     const size_t shm = (size_t)a.lds_nodes * sizeof(bvh_node32);
-    const int grid = std::max(1, blocks_per_cu(fn, rtwf::kFastBlock, shm)) * cus;
+    const int grid = grid_blocks(fn, rtwf::kFastBlock, shm, cus);
     hipLaunchKernelGGL((k_fast<FF, LST>), dim3(grid), dim3(rtwf::kFastBlock), shm, st, a);
 }
 template <int FF, bool LL>
@@ -2817,7 +2837,7 @@ void launch_fast_sort_t(bool probe, std::string* name, int cus, hipStream_t st, 
     if (name) *name = kname("k_fast_sort", FF, -1, LL ? 1 : 0);
     if (probe) return;
     const size_t shm = LL ? bytes : 0;
-    const int grid = std::max(1, blocks_per_cu(reinterpret_cast<const void*>(&k_fast_sort<FF, LL>), kSortBlock, shm)) * cus;
+    const int grid = grid_blocks(reinterpret_cast<const void*>(&k_fast_sort<FF, LL>), kSortBlock, shm, cus);
     hipLaunchKernelGGL((k_fast_sort<FF, LL>), dim3(grid), dim3(kSortBlock), shm, st, A, base, bytes);
 }
 // RTW_FAST_SORT=0: list scenes take k_fast too (A/B)
@@ -3150,15 +3170,21 @@ int rtw_handle_add_device(void* handle, double* dst, const double* src, size_t n
     return RTW_OK;
 }
 
+// A device accumulator must be memory the scene's GPU can address: device
+// memory of that GPU (hipMalloc, torch's caching and expandable-segment
+// allocators) or managed memory (hipMallocManaged: any GPU).  Host memory,
+// pinned host memory and unknown pointers are refused (a host pointer is
+// passed with accum_on_device = 0 instead).
 int rtw_check_device_ptr(const void* p, int device, const char* what) {
     hipPointerAttribute_t a;
     std::memset(&a, 0, sizeof a);
-    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeDevice) {
+    if (hipPointerGetAttributes(&a, p) != hipSuccess ||
+        (a.type != hipMemoryTypeDevice && a.type != hipMemoryTypeManaged)) {
         (void)hipGetLastError();  // clear the sticky error of a failed query
         return rtw_fail(RTW_ERR_INVALID, std::string(what) + ": accum_on_device is set but the accumulator is not "
-                                                              "device memory");
+                                                              "device or managed memory");
     }
-    if (a.device != device)
+    if (a.type == hipMemoryTypeDevice && a.device != device)
         return rtw_fail(RTW_ERR_INVALID, std::string(what) + ": the device accumulator lives on device " +
                                              std::to_string(a.device) + ", the scene on device " +
                                              std::to_string(device));

@@ -14,9 +14,11 @@ P5="WRITE_SIZE GRBM_COUNT"
 # lane utilisation (VALUUtilization = THREAD_CYCLES_VALU / (64 ACTIVE_INST_VALU))
 # and the fp32 / conversion classes of the instruction mix
 P6="SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_CVT GRBM_GUI_ACTIVE"
+# FLOP counts (lane-weighted) for the fp64 / fp32 FLOP rate against the vector peaks
+P7="SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_IOPS GRBM_GUI_ACTIVE"
 i=1
 dirs=()
-for grp in "$P1" "$P2" "$P3" "$P4" "$P5" "$P6"; do
+for grp in "$P1" "$P2" "$P3" "$P4" "$P5" "$P6" "$P7"; do
     scripts/prof_pmc.sh "${tag}_$i" "$grp" "$@"
     dirs+=("gpurun_out/pmc_${tag}_$i")
     i=$((i+1))

@@ -70,6 +70,30 @@ __global__ __launch_bounds__(256) void k_rate(double* out, unsigned seed) {
         if (K == 19) { BODY8(FMIN3) }
         if (K == 20) { BODY8(DMIN) }
         if (K == 21) { BODY8(CVTF) }
+#define FRCP(i) asm volatile("v_rcp_f32 %0, %0" : "+v"(f[i]));
+#define FSQRT(i) asm volatile("v_sqrt_f32 %0, %0" : "+v"(f[i]));
+#define FEXP(i) asm volatile("v_exp_f32 %0, %0" : "+v"(f[i]));
+#define FSIN(i) asm volatile("v_sin_f32 %0, %0" : "+v"(f[i]));
+#define MOV32(i) asm volatile("v_mov_b32 %0, %0" : "+v"(u[i]));
+#define FCMP(i) asm volatile("v_cmp_lt_f32 s[40:41], %0, %0" :: "v"(f[i]) : "s40", "s41");
+#define CNDS(i) asm volatile("v_cndmask_b32 %0, %0, %0, s[42:43]" : "+v"(u[i]) :: "s42", "s43");
+#define AND32(i) asm volatile("v_and_b32 %0, %0, %0" : "+v"(u[i]));
+#define LSHL(i) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(u[i]));
+#define DSQRT(i) asm volatile("v_sqrt_f64 %0, %0" : "+v"(d[i]));
+#define PKMUL(i) asm volatile("v_pk_mul_f32 %0, %0, %0" : "+v"(d[i]));
+#define BFE(i) asm volatile("v_bfe_u32 %0, %0, 3, 7" : "+v"(u[i]));
+        if (K == 22) { BODY8(FRCP) }
+        if (K == 23) { BODY8(FSQRT) }
+        if (K == 24) { BODY8(FEXP) }
+        if (K == 25) { BODY8(FSIN) }
+        if (K == 26) { BODY8(MOV32) }
+        if (K == 27) { BODY8(FCMP) }
+        if (K == 28) { BODY8(CNDS) }
+        if (K == 29) { BODY8(AND32) }
+        if (K == 30) { BODY8(LSHL) }
+        if (K == 31) { BODY8(DSQRT) }
+        if (K == 32) { BODY8(PKMUL) }
+        if (K == 33) { BODY8(BFE) }
     }
     double s = 0;
     for (int i = 0; i < 8; ++i) s += d[i] + (double)u[i] + (double)w[i] + (double)f[i];
@@ -80,7 +104,9 @@ static const char* kNames[] = {"v_fma_f64", "v_mul_f64", "v_add_f64", "v_rcp_f64
                                "v_div_fixup_f64", "v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32",
                                "v_mul_u32_u24", "v_add_u32", "v_cvt_f64_u32", "v_mov_b64", "v_cmp_lt_f64",
                                "v_cndmask_b32", "v_add_f32", "v_fma_f32", "v_pk_fma_f32",
-                               "v_min3_f32", "v_min_f64", "v_cvt_f32_f64"};
+                               "v_min3_f32", "v_min_f64", "v_cvt_f32_f64", "v_rcp_f32", "v_sqrt_f32",
+                               "v_exp_f32", "v_sin_f32", "v_mov_b32", "v_cmp_lt_f32", "v_cndmask_b32 (sgpr)",
+                               "v_and_b32", "v_lshlrev_b32", "v_sqrt_f64", "v_pk_mul_f32", "v_bfe_u32"};
 
 template <int K>
 static int run(double* out, int cus, double clk_ghz) {
@@ -120,6 +146,12 @@ int main() {
     run<16>(out, p.multiProcessorCount, clk); run<17>(out, p.multiProcessorCount, clk);
     run<18>(out, p.multiProcessorCount, clk); run<19>(out, p.multiProcessorCount, clk);
     run<20>(out, p.multiProcessorCount, clk); run<21>(out, p.multiProcessorCount, clk);
+    run<22>(out, p.multiProcessorCount, clk); run<23>(out, p.multiProcessorCount, clk);
+    run<24>(out, p.multiProcessorCount, clk); run<25>(out, p.multiProcessorCount, clk);
+    run<26>(out, p.multiProcessorCount, clk); run<27>(out, p.multiProcessorCount, clk);
+    run<28>(out, p.multiProcessorCount, clk); run<29>(out, p.multiProcessorCount, clk);
+    run<30>(out, p.multiProcessorCount, clk); run<31>(out, p.multiProcessorCount, clk);
+    run<32>(out, p.multiProcessorCount, clk); run<33>(out, p.multiProcessorCount, clk);
     CHK(hipFree(out));
     return 0;
 }

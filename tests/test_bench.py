@@ -55,24 +55,73 @@ def test_pmc_record_must_match_kernel_build_and_workload(bench, monkeypatch, tmp
     a = parse(bench, monkeypatch)
     assert bench.pmc_key(a) == "cornell_box 800x800 depth 50"
 
-    # the roofline: VALU-bound with the record, HBM-only without
+    # the roofline: the 8(d) HBM headline always; with the record its traffic
+    # and the bounded VALU figures beside it
     monkeypatch.setattr(bench, "PMC_DIR", tmp_path)
     monkeypatch.setattr(bench.find_pmc, "__defaults__", (tmp_path,))
     r = bench.roofline(a, rec["kernel"], "abc", seg=2e9, ms=100.0, launches=2, algo=68 * 2e9)
-    assert r["bound"] == "valu" and r["traffic"] == 1e9
-    assert abs(r["achieved"] - 1000.0 * 1e9 / 64 / 0.05 / 1e9) < 1e-6 and r["unit"] == "G wave-instr/s"
-    # a record with measured busy cycles and lane utilisation: the measured form
-    rec2 = dict(rec, valu_busy_cycles_per_segment=50.0, valu_lane_util=0.5)
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["traffic"] == 1e9
+    assert r["achieved"] == round(68 * 2e9 / 0.1 / 1e9, 2) and r["frac"] == round(r["achieved"] / 8000.0, 4)
+    assert "class_weighted" not in r["valu"]  # the record holds no instruction classes
+    # a record with class-weighted cycles, FLOPs and lane utilisation
+    rec2 = dict(rec, valu_class_cycles_per_segment=50.0, valu_lane_util=0.5, fp64_flops_per_segment=400.0,
+                write_bytes_per_launch=5e8)
     (tmp_path / "T.json").write_text(json.dumps(rec2))
     r3 = bench.roofline(a, rec["kernel"], "abc", seg=2e9, ms=100.0, launches=2, algo=68 * 2e9)
-    assert r3["unit"] == "G SIMD-cycles/s" and r3["peak"] == 1024 * 2.4
-    assert abs(r3["achieved"] - 50.0 * 1e9 / 0.05 / 1e9) < 1e-6
-    assert abs(r3["frac"] - round(1000.0 / 2457.6, 4)) < 1e-9 and r3["valu_lane_util"] == 0.5
-    assert abs(r3["valu_useful_frac"] - round(1000.0 / 2457.6 * 0.5, 4)) < 1e-9
-    assert abs(r3["issue_model"]["achieved"] - 1000.0 * 1e9 / 64 / 0.05 / 1e9) < 1e-6
-    assert r["hbm"]["achieved"] == round(68 * 2e9 / 0.1 / 1e9, 2)
+    cw = r3["valu"]["class_weighted"]
+    assert cw["unit"] == "G SIMD-cycles/s" and cw["peak"] == 1024 * 2.4
+    assert abs(cw["achieved"] - 50.0 * 1e9 / 0.05 / 1e9) < 1e-6
+    assert abs(cw["frac"] - round(1000.0 / 2457.6, 4)) < 1e-9 and r3["valu"]["lane_util"] == 0.5
+    assert abs(r3["valu"]["useful_frac"] - round(1000.0 / 2457.6 * 0.5, 4)) < 1e-9
+    fl = r3["valu"]["fp64_flops"]
+    assert abs(fl["achieved"] - 400.0 * 1e9 / 0.05 / 1e12) < 1e-9 and fl["peak"] == 78.6
+    assert r3["write_bytes"] == 5e8
     r2 = bench.roofline(a, rec["kernel"], "stale", seg=2e9, ms=100.0, launches=2, algo=68 * 2e9)
-    assert r2["bound"] == "hbm" and r2["traffic"] is None and "no PMC record" in r2["pmc"]
+    assert r2["bound"] == "hbm" and r2["traffic"] is None and "no PMC record" in r2["pmc"] and "valu" not in r2
+    # a fraction above 1 is refused, never reported
+    rec4 = dict(rec2, valu_class_cycles_per_segment=5000.0)
+    (tmp_path / "T.json").write_text(json.dumps(rec4))
+    with pytest.raises(ValueError, match="not a roofline fraction"):
+        bench.roofline(a, rec["kernel"], "abc", seg=2e9, ms=100.0, launches=2, algo=68 * 2e9)
+
+
+def test_pmc_derivation_is_bounded(monkeypatch):
+    """scripts/pmc_to_json.derive: class-weighted cycles from the instruction
+    classes (unclassified VALU at the cheapest rate), FLOPs per traversal; a
+    record missing a class gives no class-weighted figure."""
+    monkeypatch.syspath_prepend(str(ROOT / "scripts"))
+    import importlib
+    import bench as b
+    import pmc_to_json as p
+    importlib.reload(p)
+    per = {"SQ_INSTS_VALU": 1000.0, "SQ_ACTIVE_INST_VALU": 100.0, "SQ_THREAD_CYCLES_VALU": 3200.0,
+           "SQ_INSTS_VALU_FLOPS_FP64": 6400.0, "SQ_INSTS_VALU_FLOPS_FP64_TRANS": 64.0,
+           "FETCH_SIZE": 1.0, "WRITE_SIZE": 2.0}
+    per.update({f"SQ_INSTS_VALU_{k}": 50.0 for k in b.VALU_COST})
+    d = p.derive(per, 640.0)  # 10 wave-segments
+    other = 1000.0 - 50.0 * len(b.VALU_COST)
+    want = (sum(50.0 * c for c in b.VALU_COST.values()) + b.VALU_COST_OTHER * other) / 64 / 10
+    assert abs(d["valu_class_cycles_per_segment"] - want) < 1e-9
+    assert d["fp64_flops_per_segment"] == 6464.0 / 640.0 and d["valu_lane_util"] == 0.5
+    assert d["hbm_bytes_per_launch"] == 2048 + 2048
+    del per["SQ_INSTS_VALU_CVT"]
+    assert p.derive(per, 640.0)["valu_class_cycles_per_segment"] is None
+
+
+def test_committed_records_stay_below_peak(bench):
+    """Every committed PMC record, priced at its own launch time, gives
+    class-weighted VALU and fp64 FLOP fractions of at most 1."""
+    d = ROOT / "profiles" / "pmc"
+    for f in sorted(d.glob("*.json")) if d.is_dir() else []:
+        p = json.loads(f.read_text())
+        ms = p.get("avg_launch_ms")
+        if not ms:
+            continue
+        secs = ms * 1e-3
+        if p.get("valu_class_cycles_per_segment"):
+            assert p["valu_class_cycles_per_segment"] * p["segments_per_launch"] / secs / 1e9 <= bench.VALU_SIMD_GCYC, f.name
+        if p.get("fp64_flops_per_segment"):
+            assert p["fp64_flops_per_segment"] * p["segments_per_launch"] / secs / 1e12 <= bench.FP64_PEAK_TFLOPS, f.name
 
 
 def test_committed_pmc_records_are_complete():
