@@ -40,6 +40,10 @@ DEVICE = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
 HOST_SOURCES = sorted((CSRC / "host").glob("*.cpp"))
 DEVICE_SOURCES = sorted(CSRC.glob("*.hip"))
 HEADERS = sorted(list(CSRC.rglob("*.h")) + [ROOT / "include" / "rtw_gpu.h"])
+# what the device sources include: the build id and the kernels' rebuilds
+# follow these only (the host scene API headers under csrc/host/rtw/ do not
+# reach the kernels)
+DEVICE_HEADERS = sorted([*CSRC.glob("rtw_*.h"), CSRC / "host" / "rtw_host_util.h", ROOT / "include" / "rtw_gpu.h"])
 # RCCL for rtw_render_multi (multi.cpp); the same librccl.so.1 torch loads
 LIBS = ["-L/opt/rocm/lib", "-lrccl"]
 
@@ -48,7 +52,7 @@ def build_id(extra=()) -> str:
     """Hash of the device code: kernel sources, headers and compile flags
     (compiled in as RTW_BUILD_ID; bench.py matches PMC files against it)."""
     h = hashlib.sha1()
-    for f in [*DEVICE_SOURCES, *HEADERS]:
+    for f in [*DEVICE_SOURCES, *DEVICE_HEADERS]:
         h.update(f.name.encode())
         h.update(f.read_bytes())
     h.update(" ".join([*DEVICE, *COMMON, *extra]).encode())
@@ -71,7 +75,8 @@ def _run(cmd):
 
 def _compile(src: Path, force: bool, extra=(), tag: str = "") -> Path:
     obj = BUILD / (src.name + tag + ".o")
-    if force or _newer(obj, [src, *HEADERS, Path(__file__)]):
+    deps = DEVICE_HEADERS if src.suffix == ".hip" else HEADERS
+    if force or _newer(obj, [src, *deps, Path(__file__)]):
         if src.suffix == ".hip":
             bid = f'-DRTW_BUILD_ID="{build_id(extra)}"'
             cmd = [HIPCC, *DEVICE, *COMMON, *extra, bid, *INCLUDES, "-x", "hip", "-c", str(src), "-o", str(obj)]

@@ -1,14 +1,19 @@
-// hittable.h surface of the host scene API (reference hittable.h:31-489).
+// hittable.h surface of the host scene API (reference hittable.h:16-489).
 //
-// The classes keep the reference's names, constructor signatures and public
-// fields, so scene code written against the reference compiles unchanged.
-// They describe geometry; closest-hit queries (hit) are answered by the
-// device kernels after rtw_flatten_scene() has turned the graph into an
-// rtw_scene_desc.  bounding_box() keeps the reference's results (including
-// the +-0.0001f rect slabs and rotate_y's rotated corner box), and the light
-// sampling surface pdf_value() / random() (hittable.h:36-37, the xz_rect,
-// sphere and hittable_list overrides) is evaluated on the host with the
-// reference's arithmetic for pdf.h's hittable_pdf.
+// The classes keep the reference's names, constructor signatures, public
+// fields and virtual interface (hit, bounding_box, pdf_value, random), so
+// scene and tool code written against the reference compiles unchanged and
+// can be evaluated on the host: hit() answers closest-hit queries with the
+// reference's comparisons and arithmetic (IEEE fp64, the same operation
+// order), which is what tests/cpp/host_render.cpp's recursive color() runs on.
+// Renders never call these: rtw_flatten() turns the graph into an
+// rtw_scene_desc and the device kernels answer the same queries
+// (raytracingweekend_amd/csrc/rtw_device.h).
+//
+// bounding_box() keeps the reference's results (including the +-0.0001f rect
+// slabs and rotate_y's rotated corner box); pdf_value() / random() are the
+// light-sampling surface pdf.h's hittable_pdf calls (xz_rect, sphere and
+// hittable_list override them).
 #pragma once
 #include <cfloat>
 #include <cmath>
@@ -16,24 +21,69 @@
 #include <memory>
 #include <vector>
 #include "aabb.h"
-#include "material.h"
 #include "onb.h"
+#include "texture.h"
 #include "utility.h"
+
+class material;
+
+// hittable.h:16-29.  mat_ptr is borrowed from the hittable that was hit.
+struct hit_record {
+    double t = 0;
+    vec3 p;
+    vec3 normal;  // unit length for the reference's shapes (a hollow sphere's points inward)
+    double u = 0;
+    double v = 0;
+    material* mat_ptr = nullptr;
+};
 
 class hittable {
 public:
     virtual ~hittable() {}
+    // closest hit with t in the shape's accepted range below t_max (spheres:
+    // t_min < t < t_max; rects: t_min <= t <= t_max, so a rect at exactly
+    // t_max is a hit -- the tie rule of hittable_list::hit)
+    virtual bool hit(const ray& r, double t_min, double t_max, hit_record& rec) const = 0;
     virtual bool bounding_box(double t0, double t1, aabb& box) const = 0;
     // hittable.h:36-37: the defaults for objects that are not light shapes
     virtual double pdf_value(const vec3& o, const vec3& v) const { return 0.0; }
     virtual vec3 random(const vec3& o) const { return vec3(1, 0, 0); }
 };
 
+namespace rtw {
+// The axis-aligned rectangle of xy_rect / xz_rect / yz_rect (hittable.h:
+// 149-165, 184-200, 241-257): the plane coordinate K = k over [a0, a1] x
+// [b0, b1] in the axes A, B; t outside [t_lo, t_hi] or a point outside the
+// patch (bounds inclusive) misses; uv across the patch; normal +K.
+template <int A, int B, int K>
+inline bool patch_hit(const ray& r, double t_lo, double t_hi, double a0, double a1, double b0, double b1, double k,
+                      material* m, hit_record& rec) {
+    const vec3 o = r.origin(), d = r.direction();
+    const double t = (k - o[K]) / d[K];
+    if (t < t_lo || t > t_hi) return false;
+    const double a = o[A] + t * d[A];
+    const double b = o[B] + t * d[B];
+    if (a < a0 || a > a1 || b < b0 || b > b1) return false;
+    rec.u = (a - a0) / (a1 - a0);
+    rec.v = (b - b0) / (b1 - b0);
+    rec.t = t;
+    rec.mat_ptr = m;
+    rec.p = r.point_at_parameter(t);
+    vec3 n(0, 0, 0);
+    n[K] = 1;
+    rec.normal = n;
+    return true;
+}
+}  // namespace rtw
+
 class xy_rect : public hittable {
 public:
     xy_rect() {}
     xy_rect(double _x0, double _x1, double _y0, double _y1, double _k, std::shared_ptr<material> mat)
         : x0(_x0), x1(_x1), y0(_y0), y1(_y1), k(_k), mp(mat) {}
+    bool hit(const ray& r, double t0, double t1, hit_record& rec) const override {
+        return rtw::patch_hit<0, 1, 2>(r, t0, t1, x0, x1, y0, y1, k, mp.get(), rec);
+    }
     bool bounding_box(double, double, aabb& box) const override {
         box = aabb(vec3(x0, y0, k - 0.0001f), vec3(x1, y1, k + 0.0001f));
         return true;
@@ -47,23 +97,21 @@ public:
     xz_rect() {}
     xz_rect(double _x0, double _x1, double _z0, double _z1, double _k, std::shared_ptr<material> mat)
         : x0(_x0), x1(_x1), z0(_z0), z1(_z1), k(_k), mp(mat) {}
+    bool hit(const ray& r, double t0, double t1, hit_record& rec) const override {
+        return rtw::patch_hit<0, 2, 1>(r, t0, t1, x0, x1, z0, z1, k, mp.get(), rec);
+    }
     bool bounding_box(double, double, aabb& box) const override {
         box = aabb(vec3(x0, k - 0.0001f, z0), vec3(x1, k + 0.0001f, z1));
         return true;
     }
     // hittable.h:208-222: the solid-angle density of a hit of the rect along
-    // v, through xz_rect::hit (:184-200) on a ray of time FLT_MAX, t in
-    // (0.001, +inf]
+    // v, through hit() on a ray of time FLT_MAX, t in [0.001, +inf]
     double pdf_value(const vec3& origin, const vec3& v) const override {
-        const ray r(origin, v, FLT_MAX);
-        const double t = (k - r.origin().y) / r.direction().y;
-        if (t < 0.001 || t > std::numeric_limits<double>::infinity()) return 0;
-        const double x = r.origin().x + t * r.direction().x;
-        const double z = r.origin().z + t * r.direction().z;
-        if (x < x0 || x > x1 || z < z0 || z > z1) return 0;
+        hit_record rec;
+        if (!hit(ray(origin, v, FLT_MAX), 0.001, std::numeric_limits<double>::infinity(), rec)) return 0;
         const double area = (x1 - x0) * (z1 - z0);
-        const double distance_squared = t * t * v.length_squared();
-        const double cosine = std::fabs(dot(v, vec3(0, 1, 0)) / v.length());
+        const double distance_squared = rec.t * rec.t * v.length_squared();
+        const double cosine = std::fabs(dot(v, rec.normal) / v.length());
         return distance_squared / (cosine * area);
     }
     // hittable.h:224-228 (z drawn first, as g++ evaluates the vec3 arguments)
@@ -81,6 +129,9 @@ public:
     yz_rect() {}
     yz_rect(double _y0, double _y1, double _z0, double _z1, double _k, std::shared_ptr<material> mat)
         : y0(_y0), y1(_y1), z0(_z0), z1(_z1), k(_k), mp(mat) {}
+    bool hit(const ray& r, double t0, double t1, hit_record& rec) const override {
+        return rtw::patch_hit<1, 2, 0>(r, t0, t1, y0, y1, z0, z1, k, mp.get(), rec);
+    }
     bool bounding_box(double, double, aabb& box) const override {
         box = aabb(vec3(k - 0.0001f, y0, z0), vec3(k + 0.0001f, y1, z1));
         return true;
@@ -89,16 +140,29 @@ public:
     std::shared_ptr<material> mp;
 };
 
+// hittable.h:273-284: the child's hit with the normal reversed
 class flip_normals : public hittable {
 public:
     flip_normals(std::shared_ptr<hittable> p) : ptr(p) {}
+    bool hit(const ray& r, double t0, double t1, hit_record& rec) const override {
+        if (!ptr->hit(r, t0, t1, rec)) return false;
+        rec.normal = -rec.normal;
+        return true;
+    }
     bool bounding_box(double t0, double t1, aabb& box) const override { return ptr->bounding_box(t0, t1, box); }
     std::shared_ptr<hittable> ptr;
 };
 
+// hittable.h:299-311: the ray moves by -offset, the hit point back by +offset
 class translate : public hittable {
 public:
     translate(std::shared_ptr<hittable> p, const vec3& displacement) : ptr(p), offset(displacement) {}
+    bool hit(const ray& r, double t0, double t1, hit_record& rec) const override {
+        const ray moved(r.origin() - offset, r.direction(), r.time());
+        if (!ptr->hit(moved, t0, t1, rec)) return false;
+        rec.p += offset;
+        return true;
+    }
     bool bounding_box(double t0, double t1, aabb& box) const override {
         if (!ptr->bounding_box(t0, t1, box)) return false;
         box = aabb(box.min() + offset, box.max() + offset);
@@ -108,9 +172,21 @@ public:
     vec3 offset;
 };
 
+// hittable.h:314-415: the ray turns by -angle about +y into the child's
+// frame; the hit point and normal turn back by +angle
 class rotate_y : public hittable {
 public:
     rotate_y(std::shared_ptr<hittable> p, double angle);
+    bool hit(const ray& r, double t_min, double t_max, hit_record& rec) const override {
+        const vec3 o = r.origin(), d = r.direction();
+        const vec3 o_local(cos_theta * o[0] - sin_theta * o[2], o[1], sin_theta * o[0] + cos_theta * o[2]);
+        const vec3 d_local(cos_theta * d[0] - sin_theta * d[2], d[1], sin_theta * d[0] + cos_theta * d[2]);
+        if (!ptr->hit(ray(o_local, d_local, r.time()), t_min, t_max, rec)) return false;
+        const vec3 p = rec.p, n = rec.normal;
+        rec.p = vec3(cos_theta * p[0] + sin_theta * p[2], p[1], -sin_theta * p[0] + cos_theta * p[2]);
+        rec.normal = vec3(cos_theta * n[0] + sin_theta * n[2], n[1], -sin_theta * n[0] + cos_theta * n[2]);
+        return true;
+    }
     bool bounding_box(double, double, aabb& box) const override {
         box = bbox;
         return hasbox;
@@ -122,10 +198,35 @@ public:
     aabb bbox;
 };
 
+// hittable.h:420-479: a volume of constant density inside `boundary`.  The
+// free-flight distance -(1/density) log(U) is drawn on every call, from the
+// function's own engine (the thread's path stream while one is open) -- so
+// under hittable_list::hit's double walk a medium draws twice per query
+// (SURVEY.md A.3), as in the reference.
 class constant_medium : public hittable {
 public:
     constant_medium(std::shared_ptr<hittable> b, double d, std::shared_ptr<material> mat)
         : boundary(b), density(d), mp(mat) {}
+    bool hit(const ray& r, double t_min, double t_max, hit_record& rec) const override {
+        static std::uniform_real_distribution<double> uniform;
+        static rtw::engine engine;
+        const double far = std::numeric_limits<double>::max();
+        hit_record in, out;
+        if (!boundary->hit(r, -far, far, in)) return false;
+        if (!boundary->hit(r, in.t + 0.0001f, far, out)) return false;
+        in.t = in.t < t_min ? t_min : in.t;
+        out.t = out.t > t_max ? t_max : out.t;
+        if (in.t >= out.t) return false;
+        if (in.t < 0) in.t = 0;
+        const double inside = (out.t - in.t) * r.direction().length();
+        const double travel = -(1 / density) * std::log(uniform(engine));
+        if (!(travel < inside)) return false;
+        rec.t = in.t + travel / r.direction().length();
+        rec.p = r.point_at_parameter(rec.t);
+        rec.normal = vec3(1, 0, 0);  // arbitrary: isotropic scattering ignores it
+        rec.mat_ptr = mp.get();
+        return true;
+    }
     bool bounding_box(double t0, double t1, aabb& box) const override { return boundary->bounding_box(t0, t1, box); }
     std::shared_ptr<hittable> boundary;
     double density;
@@ -134,18 +235,37 @@ public:
 
 // bvh_node: the reference's version (hittable.h:41-140) never assigns `right`,
 // tests `left` twice and sorts n-1 elements, and no scene uses
-// it.  Here it is a correct container: its objects are flattened as a group
-// and the library builds a device BVH over them, whose closest hit equals the
-// flat hittable_list's (same comparison operators and tie order).
+// it.  Here it is a correct BVH over `objects` (scene_api.cpp builds a
+// median-split tree of their boxes) whose hit() returns exactly what a
+// hittable_list of the same objects returns: the closest distance is found by
+// a nearest-first walk, then the objects whose boxes reach it are run through
+// hittable_list::hit's double walk in list order, so the reference's tie rule
+// (the last object accepting a hit at exactly the closest t; else the first
+// one reaching it) picks the same record.  Media draw in that order too (the
+// flattener refuses a bvh_node holding one: the reference's own walk order
+// cannot be reproduced, A.1).  The device builds its own BVH for renders.
 class bvh_node : public hittable {
 public:
     bvh_node() {}
     bvh_node(hittable** l, int n, double time0, double time1);
     bvh_node(const std::vector<std::shared_ptr<hittable>>& l, double time0, double time1);
+    bool hit(const ray& r, double t_min, double t_max, hit_record& rec) const override;
     bool bounding_box(double, double, aabb& b) const override {
         b = box;
         return true;
     }
     std::vector<std::shared_ptr<hittable>> objects;
     aabb box;
+
+    // the tree: node 0 is the root; a leaf holds objects [first, first + count)
+    // of `order` (indices into `objects`), an inner node its two children
+    struct node {
+        aabb bounds;
+        int first = 0, count = 0, left = -1, right = -1;
+    };
+    std::vector<node> nodes;
+    std::vector<int> order;
+
+private:
+    void build(double time0, double time1);
 };

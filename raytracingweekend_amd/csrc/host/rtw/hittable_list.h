@@ -1,11 +1,31 @@
 // hittable_list.h surface of the host scene API (reference hittable_list.h:5-114).
 #pragma once
+#include "material.h"
 #include "sphere.h"
 
 class hittable_list : public hittable {
 public:
     hittable_list() {}
     hittable_list(const std::vector<std::shared_ptr<hittable>>& l) : objects(l) {}
+    // hittable_list.h:11-37: closest hit over the objects, walked TWICE with
+    // the closest distance carried over.  For deterministic shapes the second
+    // walk re-accepts only hits at exactly that distance (rects: t == t_max
+    // is accepted), so ties go to the last such object; a medium draws a
+    // fresh free-flight distance in each walk.
+    bool hit(const ray& r, double t_min, double t_max, hit_record& rec) const override {
+        hit_record cand;
+        bool any = false;
+        double closest = t_max;
+        for (int walk = 0; walk < 2; ++walk) {
+            for (const auto& object : objects) {
+                if (!object->hit(r, t_min, closest, cand)) continue;
+                any = true;
+                closest = cand.t;
+                rec = cand;
+            }
+        }
+        return any;
+    }
     // As the reference (hittable_list.h:39-42): reports true without setting `box`.
     bool bounding_box(double, double, aabb&) const override { return true; }
     // hittable_list.h:44-53: the members' densities, equally weighted
@@ -29,6 +49,8 @@ class box : public hittable {
 public:
     box() {}
     box(const vec3& p0, const vec3& p1, std::shared_ptr<material> mat);
+    // hittable_list.h:106-110: the six rects' list (its own double walk)
+    bool hit(const ray& r, double t0, double t1, hit_record& rec) const override { return list_ptr.hit(r, t0, t1, rec); }
     bool bounding_box(double, double, aabb& b) const override {
         b = aabb(pmin, pmax);
         return true;

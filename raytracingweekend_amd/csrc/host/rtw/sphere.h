@@ -1,6 +1,7 @@
 // sphere.h surface of the host scene API (reference sphere.h:6-131).
 #pragma once
 #include "hittable.h"
+#include "material.h"
 
 struct movement_none {
     vec3 center(const vec3& center0, double) const { return center0; }
@@ -30,6 +31,30 @@ class sphere_base : public hittable {
 public:
     sphere_base() : center(0, 0, 0), radius(0), mat(nullptr) {}
     sphere_base(vec3 cen, double r, std::shared_ptr<material> m) : center(cen), radius(r), mat(m) {}
+    // sphere.h:46-81: the half-b quadratic about the centre at the ray's
+    // time; the near root, else the far one, strictly inside (t_min, t_max);
+    // normal (p - c) / radius (inward for a negative radius: hollow glass)
+    bool hit(const ray& r, double t_min, double t_max, hit_record& rec) const override {
+        const vec3 c_now = movement.center(center, r.time());
+        const vec3 oc = r.origin() - c_now;
+        const double a = dot(r.direction(), r.direction());
+        const double b = dot(oc, r.direction());
+        const double c = dot(oc, oc) - radius * radius;
+        const double disc = b * b - a * c;
+        if (!(disc > 0)) return false;
+        for (int side = -1; side <= 1; side += 2) {
+            const double root = (-b + side * std::sqrt(disc)) / a;
+            if (root < t_max && root > t_min) {
+                rec.t = root;
+                rec.p = r.point_at_parameter(root);
+                rec.normal = (rec.p - c_now) / radius;
+                get_sphere_uv(rec.normal, rec.u, rec.v);
+                rec.mat_ptr = mat.get();
+                return true;
+            }
+        }
+        return false;
+    }
     bool bounding_box(double t0, double t1, aabb& box) const override {
         return movement.bounding_box(center, radius, t0, t1, box);
     }
@@ -37,21 +62,9 @@ public:
 
     // sphere.h:88-99: uniform density over the cone the sphere subtends,
     // where a ray of time FLT_MAX along v hits it in (0.001, +inf)
-    // (sphere.h:46-81's roots about the centre at that time)
     double pdf_value(const vec3& o, const vec3& v) const override {
-        const ray r(o, v, FLT_MAX);
-        const vec3 oc = r.origin() - movement.center(center, r.time());
-        const double a = dot(r.direction(), r.direction());
-        const double b = dot(oc, r.direction());
-        const double c = dot(oc, oc) - radius * radius;
-        const double disc = b * b - a * c;
-        const double t_max = std::numeric_limits<double>::infinity();
-        if (!(disc > 0)) return 0.0;
-        double temp = (-b - std::sqrt(disc)) / a;
-        if (!(temp < t_max && temp > 0.001)) {
-            temp = (-b + std::sqrt(disc)) / a;
-            if (!(temp < t_max && temp > 0.001)) return 0.0;
-        }
+        hit_record rec;
+        if (!hit(ray(o, v, FLT_MAX), 0.001, std::numeric_limits<double>::infinity(), rec)) return 0.0;
         const double cos_theta_max = std::sqrt(1 - radius * radius / (center - o).length_squared());
         const double solid_angle = 2.0 * M_PI * (1.0 - cos_theta_max);
         return 1.0 / solid_angle;
@@ -64,6 +77,9 @@ public:
         uvw.build_from_w(direction);
         return uvw.local(random_to_sphere(radius, distance_squared));
     }
+
+    // sphere.h:115-122: longitude / latitude of a unit normal
+    static void get_sphere_uv(const vec3& p, double& u, double& v) { ::get_sphere_uv(p, u, v); }
 
     vec3 center;
     double radius;

@@ -1,23 +1,98 @@
 // utility.h surface of the host scene API (reference utility.h:6-81): the
 // global random_double engine and the direction samplers, for scene code
-// written against the reference (random_balls-style layouts, custom pdfs).
+// written against the reference (random_balls-style layouts, custom pdfs),
+// and the engines the host classes' hit / scatter / get_ray draw from.
 //
-// Host only.  Renders draw on the device from per-sample streams
-// (rtw_path_seed) with these same formulas (rtw_device.h); this engine is
-// the reference's single function-static std::minstd_rand, default seeded,
-// with libstdc++'s generate_canonical<double, 53> (two raw draws per double).
+// Every engine of the host API (random_double's, the dielectric's and the
+// medium's function-static ones, the camera's two members, a render loop's
+// own) is an rtw::engine: std::minstd_rand's recurrence and range, default
+// seed 1, consumed by libstdc++'s generate_canonical<double, 53> as two raw
+// draws per double.  While an rtw::path_stream is alive on a thread, every
+// rtw::engine on that thread draws from that stream instead: the per-sample
+// stream of include/rtw_gpu.h (rtw_path_seed(seed, pixel, sample)), which is
+// what the device kernels draw from, so a host render that opens one stream
+// per camera sample reproduces the GPU's and the oracle's paths.
 // Where the reference builds vec3(random_double(), ...) from several draws,
 // g++ evaluates the arguments right to left; the draws are made explicitly in
 // that order here (z, y, x), so the values do not depend on the compiler.
 #pragma once
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <random>
 #include "vec3.h"
 
 #ifndef M_PI
 #define M_PI 3.14159265358979323846
 #endif
+
+namespace rtw {
+
+// The stream a thread's engines draw from while a path_stream is open (0: none).
+struct stream_state {
+    uint64_t x = 0;       // minstd_rand state of the open stream, 0 = no stream open
+    uint64_t draws = 0;   // raw draws taken from it
+};
+inline stream_state& current_stream() {
+    static thread_local stream_state s;
+    return s;
+}
+
+// rtw_path_seed (include/rtw_gpu.h): splitmix64 finaliser (Steele, Lea,
+// Flood 2014) of the seed, mixed with (sample << 32) ^ pixel, into [1, 2^31-2]
+inline uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+inline uint32_t path_seed(uint64_t seed, uint32_t pixel, uint32_t sample) {
+    const uint64_t key = ((uint64_t)sample << 32) ^ (uint64_t)pixel;
+    return (uint32_t)(1u + splitmix64(splitmix64(seed) ^ key) % 2147483646ull);
+}
+
+// std::minstd_rand's generator (48271 x mod 2^31 - 1), redirected to the
+// thread's open path stream when there is one.
+class engine {
+public:
+    typedef std::uint_fast32_t result_type;
+    static constexpr result_type min() { return 1; }
+    static constexpr result_type max() { return 2147483646; }
+    engine() {}
+    explicit engine(result_type s) { seed(s); }
+    void seed(result_type s = 1) {
+        state_ = s % 2147483647u;
+        if (state_ == 0) state_ = 1;
+    }
+    result_type operator()() {
+        stream_state& st = current_stream();
+        uint64_t& x = st.x ? st.x : state_;
+        if (st.x) ++st.draws;
+        x = x * 48271u % 2147483647u;
+        return (result_type)x;
+    }
+
+private:
+    uint64_t state_ = 1;
+};
+
+// Opens the per-sample stream rtw_path_seed(seed, pixel, sample) on this
+// thread for its lifetime (camera sample = one path_stream).
+class path_stream {
+public:
+    path_stream(uint64_t seed, uint32_t pixel, uint32_t sample) : saved_(current_stream()) {
+        current_stream() = stream_state{path_seed(seed, pixel, sample), 0};
+    }
+    ~path_stream() { current_stream() = saved_; }
+    uint64_t draws() const { return current_stream().draws; }
+    path_stream(const path_stream&) = delete;
+    path_stream& operator=(const path_stream&) = delete;
+
+private:
+    stream_state saved_;
+};
+
+}  // namespace rtw
 
 // utility.h:6-12 (the free function; sphere_base keeps its own copy)
 inline void get_sphere_uv(const vec3& p, double& u, double& v) {
@@ -31,7 +106,7 @@ inline void get_sphere_uv(const vec3& p, double& u, double& v) {
 // statics are shared by every translation unit)
 inline double random_double(double a = 0.0, double b = 1.0) {
     static std::uniform_real_distribution<double> uniform;
-    static std::minstd_rand engine;
+    static rtw::engine engine;
     return a + (b - a) * uniform(engine);
 }
 
