@@ -54,18 +54,19 @@ FP32_PEAK_TFLOPS = 157.3
 # Issue cost of one wave64 VALU instruction per SIMD, in cycles at the nominal
 # 2.4 GHz, per SQ_INSTS_VALU_* class: measured on the card with independent
 # chains at 4 waves/SIMD (scripts/valu_rates.hip; profiles/r01/valu_rates.log,
-# profiles/r04/valu_rates.log).  Each class takes its cheapest measured
-# member (F64: fma/mul/add 4.6, div_scale / fixup 4.6-4.8; TRANS_F64:
-# rcp/rsq 16.6-16.8; INT32: v_add_u32 2.55, v_mul_lo_u32 4.35; INT64:
-# v_mad_u64_u32 5.15; CVT: v_cvt_f64_u32 5.26, v_cvt_f32_f64 5.33; F32:
-# v_add_f32 2.60, v_fma_f32 2.70; TRANS_F32: v_rcp/v_sqrt/v_exp/v_log/v_sin
-# _f32), and instructions no class counts (moves, compares, selects, logic)
-# take the cheapest rate of all -- so the class-weighted cycles are a LOWER
-# bound of the SIMD's VALU issue time and their fraction of the SIMD cycles
-# is at most 1 when the rates hold.
-VALU_COST = {"FMA_F64": 4.59, "MUL_F64": 4.59, "ADD_F64": 4.59, "TRANS_F64": 16.6,
+# profiles/r04/valu_rates.log).  Each class takes the cheapest measured cost
+# of any of its members in either log (F64: v_fma/mul/add_f64 4.59-4.81;
+# TRANS_F64: v_sqrt_f64 16.35, v_rsq/rcp_f64 16.6-17.4; INT32: v_add_u32 /
+# v_and_b32 / v_mov_b32 2.55-2.64, v_lshlrev / v_bfe / v_mul_lo 4.3-4.4;
+# INT64: v_mad_u64_u32 5.15; CVT: v_cvt_f64_u32 5.26, v_cvt_f32_f64 5.33;
+# F32: v_add_f32 2.60, v_fma_f32 2.70, packed 4.4-4.8; TRANS_F32:
+# v_rcp/v_sqrt/v_exp/v_sin_f32 8.36-8.63), and instructions no class counts
+# (moves, compares, selects, logic: 2.6-4.5) take the cheapest rate of all
+# -- so the class-weighted cycles are a LOWER bound of the SIMDs' VALU issue
+# time, and their fraction of the SIMD cycles is at most 1.
+VALU_COST = {"FMA_F64": 4.59, "MUL_F64": 4.59, "ADD_F64": 4.59, "TRANS_F64": 16.35,
              "INT32": 2.55, "INT64": 5.15, "CVT": 5.26,
-             "FMA_F32": 2.60, "ADD_F32": 2.60, "MUL_F32": 2.60, "TRANS_F32": 4.4}
+             "FMA_F32": 2.60, "ADD_F32": 2.60, "MUL_F32": 2.60, "TRANS_F32": 8.36}
 VALU_COST_OTHER = 2.55
 PMC_DIR = ROOT / "profiles" / "pmc"
 

@@ -125,12 +125,23 @@ inline vec3 random_in_unit_sphere() {
     return p;
 }
 
+namespace rtw {
+// sin and cos of one angle.  g++ -O2 (the reference's build) turns the
+// reference's cos(phi) ... sin(phi) pairs into ONE glibc sincos() call, and
+// glibc's sincos and its separate sin / cos can differ in the last ulp; the
+// host API makes that call explicitly, so its values do not depend on the
+// compiler that builds it (clang keeps two calls).
+inline void sin_cos(double phi, double& s, double& c) { ::sincos(phi, &s, &c); }
+}  // namespace rtw
+
 // utility.h:37-43 (a before z: two statements in the reference)
 inline vec3 random_unit_vector() {
     const double a = random_double() * 2.0 * M_PI;
     const double z = random_double() * 2.0 - 1.0;
     const double r = std::sqrt(1 - z * z);
-    return vec3(r * std::cos(a), r * std::sin(a), z);
+    double s, c;
+    rtw::sin_cos(a, s, c);
+    return vec3(r * c, r * s, z);
 }
 
 // utility.h:45-52
@@ -145,8 +156,10 @@ inline vec3 random_cosine_direction() {
     const double r2 = random_double();
     const double z = std::sqrt(1 - r2);
     const double phi = 2 * M_PI * r1;
-    const double x = std::cos(phi) * std::sqrt(r2);
-    const double y = std::sin(phi) * std::sqrt(r2);
+    double s, c;
+    rtw::sin_cos(phi, s, c);
+    const double x = c * std::sqrt(r2);
+    const double y = s * std::sqrt(r2);
     return vec3(x, y, z);
 }
 
@@ -157,7 +170,9 @@ inline vec3 random_to_sphere(double radius, double distance_squared) {
     const double r2 = random_double();
     const double z = 1 + r2 * (std::sqrt(1 - radius * radius / distance_squared) - 1);
     const double phi = 2 * M_PI * r1;
-    const double x = std::cos(phi) * std::sqrt(1 - z * z);
-    const double y = std::sin(phi) * std::sqrt(1 - z * z);
+    double s, c;
+    rtw::sin_cos(phi, s, c);
+    const double x = c * std::sqrt(1 - z * z);
+    const double y = s * std::sqrt(1 - z * z);
     return vec3(x, y, z);
 }

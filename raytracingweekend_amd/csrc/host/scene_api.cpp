@@ -123,8 +123,8 @@ aabb widened(const aabb& b) {
 // the box (hittable_list.h:39-42), so a translate / rotate_y over a list
 // inherits garbage, and rotate_y rotates only two corners of its child's box
 // (hittable.h:334-372).  Lists are unioned, transforms re-derived from their
-// child's true box (all eight corners), anything unknown without a box is
-// unbounded.
+// child's true box (all eight corners), inverted boxes (negative radii)
+// reordered, anything unknown without a box is unbounded.
 bool true_box(const hittable* h, double t0, double t1, aabb& out) {
     const double inf = std::numeric_limits<double>::infinity();
     if (auto l = dynamic_cast<const hittable_list*>(h)) {
@@ -165,7 +165,13 @@ bool true_box(const hittable* h, double t0, double t1, aabb& out) {
         out = aabb(lo, hi);
         return true;
     }
-    return h->bounding_box(t0, t1, out);
+    if (!h->bounding_box(t0, t1, out)) return false;
+    // a negative radius (hollow glass) gives sphere boxes with min > max
+    vec3 lo = out.min(), hi = out.max();
+    for (int a = 0; a < 3; ++a)
+        if (lo[a] > hi[a]) std::swap(lo[a], hi[a]);
+    out = aabb(lo, hi);
+    return true;
 }
 
 // a ray's overlap with the slabs of b on [tmin, tmax], inclusive at the ends

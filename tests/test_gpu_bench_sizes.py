@@ -222,10 +222,10 @@ def test_render_multi_rejects_bad_handles_and_accumulators(gpu):
         host = np.zeros(nx * ny * 3)
         assert L.rtw_render_multi(1, hs, C.byref(sd.camera), C.byref(prm), host.ctypes.data_as(C.c_void_p),
                                   None) == -1
-        assert b"not device memory" in L.rtw_last_error()
+        assert b"not device or managed memory" in L.rtw_last_error()
         assert L.rtw_render_accumulate(a.handle, C.byref(sd.camera), C.byref(prm), host.ctypes.data_as(C.c_void_p),
                                        None) == -1
-        assert b"not device memory" in L.rtw_last_error()
+        assert b"not device or managed memory" in L.rtw_last_error()
         prm.accum_on_device, prm.precision = 0, 7
         assert L.rtw_render_accumulate(a.handle, C.byref(sd.camera), C.byref(prm), host.ctypes.data_as(C.c_void_p),
                                        None) == -1
@@ -236,6 +236,40 @@ def test_render_multi_rejects_bad_handles_and_accumulators(gpu):
         L.rtw_release_communicators()
         a.close()
         b.close()
+
+
+def test_managed_memory_accumulator(gpu):
+    """A device accumulator in managed memory (hipMallocManaged) is accepted
+    by rtw_render_accumulate and rtw_render_multi, and gives the same sums as
+    a host accumulator."""
+    import ctypes as C
+    from raytracingweekend_amd import _abi
+    hip = C.CDLL("libamdhip64.so.7")  # by soname: the runtime torch and librtw.so already share
+    nx, ny, spp = 16, 12, 2
+    n = nx * ny * 3
+    sd = gpu.SceneDesc("cornell_box", nx / ny)
+    a = gpu.DeviceScene(sd)
+    L = gpu.lib()
+    ptr = C.c_void_p()
+    assert hip.hipMallocManaged(C.byref(ptr), C.c_size_t(n * 8), C.c_uint(1)) == 0  # hipMemAttachGlobal
+    try:
+        ref, _ = a.render_accumulate(nx, ny, spp, 10, seed=4)
+        C.memset(ptr, 0, n * 8)
+        prm = _abi.rtw_render_params(nx=nx, ny=ny, spp=spp, max_depth=10, seed=4, row_step=1, accum_on_device=1)
+        _abi.check(L.rtw_render_accumulate(a.handle, C.byref(sd.camera), C.byref(prm), ptr, None), "managed")
+        assert hip.hipDeviceSynchronize() == 0
+        got = np.ctypeslib.as_array((C.c_double * n).from_address(ptr.value)).copy()
+        assert np.array_equal(got, ref)
+        C.memset(ptr, 0, n * 8)
+        hs = (C.c_void_p * 1)(a.handle.value)
+        _abi.check(L.rtw_render_multi(1, hs, C.byref(sd.camera), C.byref(prm), ptr, None), "managed multi")
+        assert hip.hipDeviceSynchronize() == 0
+        got = np.ctypeslib.as_array((C.c_double * n).from_address(ptr.value)).copy()
+        assert np.array_equal(got, ref)
+    finally:
+        hip.hipFree(ptr)
+        L.rtw_release_communicators()
+        a.close()
 
 
 @pytest.mark.skipif("not __import__('torch').cuda.is_available() or __import__('torch').cuda.device_count() < 2",
