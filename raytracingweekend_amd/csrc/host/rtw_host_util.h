@@ -18,6 +18,10 @@ T* rtw_dup(const std::vector<T>& v) {
     return p;
 }
 
+// RTW_OK when a caller's scene desc is safe to upload, else RTW_ERR_INVALID /
+// RTW_ERR_UNSUPPORTED with the reason (validate.cpp).
+int validate_desc(const rtw_scene_desc* d);
+
 // Internal entry points of the kernel translation unit (rtw_kernels.hip) for
 // the host library (multi.cpp); not part of the C ABI.
 int rtw_handle_device(void* handle);                                             // -1 for null
