@@ -5,7 +5,11 @@
 //
 //   rtw_render [--scene cornell_box] [--nx 400] [--ny 400] [--spp 64]
 //              [--depth 100] [--seed 0] [--bvh] [--device 0] [--gpus 1]
-//              [--out out.ppm]
+//              [--precision fp64|fp32] [--out out.ppm]
+//
+// --precision fp64 (default) is the parity mode (the reference's double
+// arithmetic on every path decision); fp32 the fast mode (single precision,
+// statistical parity only; rtw_render_params.precision).
 //
 // --gpus N renders on devices device .. device+N-1 from this one process
 // (rtw_render_multi: one host thread per GPU, RCCL reduce to the first).
@@ -23,7 +27,7 @@
 
 int main(int argc, char** argv) {
     std::string scene_name = "cornell_box", out = "1.ppm";
-    int nx = 400, ny = 400, spp = 64, depth = 100, device = 0, bvh = 0, gpus = 1;
+    int nx = 400, ny = 400, spp = 64, depth = 100, device = 0, bvh = 0, gpus = 1, precision = RTW_PRECISION_FP64;
     unsigned long long seed = 0;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -44,6 +48,15 @@ int main(int argc, char** argv) {
         else if (a == "--gpus") gpus = std::atoi(next());
         else if (a == "--out") out = next();
         else if (a == "--bvh") bvh = 1;
+        else if (a == "--precision") {
+            const std::string v = next();
+            if (v == "fp64") precision = RTW_PRECISION_FP64;
+            else if (v == "fp32") precision = RTW_PRECISION_FP32;
+            else {
+                std::fprintf(stderr, "--precision %s: expected fp64 or fp32\n", v.c_str());
+                return 2;
+            }
+        }
         else {
             std::fprintf(stderr, "unknown argument %s\n", a.c_str());
             return 2;
@@ -74,6 +87,7 @@ int main(int argc, char** argv) {
     rtw_render_params p;
     std::memset(&p, 0, sizeof p);
     p.nx = nx, p.ny = ny, p.spp = spp, p.max_depth = depth, p.seed = seed, p.row_step = 1;
+    p.precision = precision;
     std::vector<double> accum((size_t)nx * ny * 3, 0.0), canvas(accum.size());
     rtw_stats st;
     auto t0 = std::chrono::high_resolution_clock::now();

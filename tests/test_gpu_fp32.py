@@ -140,3 +140,20 @@ def test_node_packet_changes_no_sample(gpu, scene, precision):
     without, s0 = _render_child({"RTW_LDS_NODES": "0"}, scene, nx, ny, spp, depth, 7, True, precision)
     assert s1 == s0 and np.array_equal(with_p, without)
     assert np.all(np.isfinite(with_p)) and with_p.sum() > 0
+
+
+def test_cli_precision_switch(tmp_path):
+    """The reference-main equivalent (rtw_render) renders in either precision
+    (--precision fp64|fp32, SURVEY.md §5's config row) and writes its PPM."""
+    import subprocess
+    from raytracingweekend_amd import build
+    cli = build.CLI
+    assert cli.exists(), "rtw_render is built by raytracingweekend_amd.build (build())"
+    for prec in ("fp64", "fp32"):
+        out = tmp_path / f"{prec}.ppm"
+        r = subprocess.run([str(cli), "--scene", "cornell_box", "--nx", "32", "--ny", "32", "--spp", "4",
+                            "--depth", "20", "--precision", prec, "--out", str(out)], capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert "Msamples/s" in r.stdout
+        assert out.read_text().startswith("P3\n32 32\n255\n")

@@ -27,6 +27,8 @@ def test_cli_rejects_unknown_scene(built):
     cli = build.build_cli()
     r = subprocess.run([str(cli), "--scene", "nope"], capture_output=True, text=True)
     assert r.returncode == 2 and "unknown scene" in r.stderr
+    r = subprocess.run([str(cli), "--precision", "fp16"], capture_output=True, text=True)
+    assert r.returncode == 2 and "expected fp64 or fp32" in r.stderr
 
 
 def _minstd_canonical(n):
