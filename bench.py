@@ -247,18 +247,21 @@ def roofline(args, kernel, build, seg, ms, launches, algo):
                           "x 2.4 GHz (a lower bound of VALU issue time)"}
         if v["lane_util"]:
             v["useful_frac"] = round(ach / VALU_SIMD_GCYC * v["lane_util"], 4)
+    lane = v["lane_util"] or 1.0
     fl = rec.get("fp64_flops_per_segment")
     if fl is not None:
-        tf = fl * seg_launch / secs / 1e12
-        v["fp64_flops"] = {"achieved": round(tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(tf / FP64_PEAK_TFLOPS, 4),
-                           "definition": "SQ_INSTS_VALU_FLOPS_FP64 (+ _TRANS) per traversal x traversals / launch "
-                                         "time, against the 78.6 TF fp64 vector peak"}
+        issued = fl * seg_launch / secs / 1e12
+        v["fp64_flops"] = {"achieved": round(issued * lane, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(issued * lane / FP64_PEAK_TFLOPS, 4), "issued": round(issued, 3),
+                           "issued_frac": round(issued / FP64_PEAK_TFLOPS, 4),
+                           "definition": "SQ_INSTS_VALU_FLOPS_FP64 (per wave instruction: FMA 2, MUL / ADD / TRANS "
+                                         "1) x 64 lanes per traversal x traversals / launch time = issued; x the lane "
+                                         "utilisation = achieved; against the 78.6 TF fp64 vector peak"}
     fl32 = rec.get("fp32_flops_per_segment")
     if fl32:
-        tf = fl32 * seg_launch / secs / 1e12
-        v["fp32_flops"] = {"achieved": round(tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(tf / FP32_PEAK_TFLOPS, 4)}
+        issued = fl32 * seg_launch / secs / 1e12
+        v["fp32_flops"] = {"achieved": round(issued * lane, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(issued * lane / FP32_PEAK_TFLOPS, 4), "issued": round(issued, 3)}
     out["valu"] = v
     check_fracs(out)
     return out

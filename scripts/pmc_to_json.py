@@ -18,8 +18,9 @@ The derived figures (`derive`) are bounded:
     profiles/r04/valu_rates.log), the instructions no class counts (moves,
     compares, selects, logic) at the cheapest measured rate -- per traversal;
     bench.py divides by the launch time x 1024 SIMDs x clock;
-  * fp64_flops_per_segment: SQ_INSTS_VALU_FLOPS_FP64 (+ _TRANS) per
-    traversal, against the 78.6 TF fp64 vector peak in bench.py;
+  * fp64_flops_per_segment: SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes per
+    traversal (the counter counts per wave instruction), against the 78.6 TF
+    fp64 vector peak in bench.py, issued and lane-weighted;
   * valu_lane_util: SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU).
 SQ_ACTIVE_INST_VALU sums the cycles of every co-resident wave, so its ratio
 to the SIMD cycles is kept only as a diagnostic (valu_active_wave_sum); it can
@@ -60,12 +61,15 @@ def derive(per: dict, seg_per_launch: float) -> dict:
     # that misses one would price its instructions at the cheapest rate
     complete = valu > 0 and all(f"SQ_INSTS_VALU_{k}" in per for k in VALU_COST)
     cycles = sum(VALU_COST[k] * v for k, v in classes.items()) + VALU_COST_OTHER * other
+    # SQ_INSTS_VALU_FLOPS_FP64 counts per WAVE instruction (FMA 2, MUL / ADD /
+    # TRANS 1; _TRANS is a subset): measured, it equals 2 FMA_F64 + MUL_F64 +
+    # ADD_F64 + TRANS_F64 (profiles/pmc/T_r4a.json).  x 64 lanes = the FLOPs
+    # the issued instructions could do with every lane on (an upper bound);
+    # bench.py weights it by the lane utilisation for the useful rate.
     flops64 = per.get("SQ_INSTS_VALU_FLOPS_FP64")
-    if flops64 is not None:
-        flops64 += per.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0)
+    flops64 = flops64 * 64 if flops64 is not None else None
     flops32 = per.get("SQ_INSTS_VALU_FLOPS_FP32")
-    if flops32 is not None:
-        flops32 += per.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0.0)
+    flops32 = flops32 * 64 if flops32 is not None else None
     gui = per.get("GRBM_GUI_ACTIVE")
     act = per.get("SQ_ACTIVE_INST_VALU")
     cyc = per.get("SQ_WAVE_CYCLES", 0) or 1
@@ -87,7 +91,7 @@ def derive(per: dict, seg_per_launch: float) -> dict:
         # (i) class-weighted VALU issue cycles of one SIMD per traversal
         "valu_class_cycles_per_segment": cycles / 64 / wave_segments if (wave_segments and complete) else None,
         "valu_class_complete": complete,
-        # (ii) fp64 / fp32 FLOPs per traversal (lane-weighted by the counter)
+        # (ii) fp64 / fp32 FLOPs per traversal issued (64 lanes per instruction)
         "fp64_flops_per_segment": flops64 / seg_per_launch if (flops64 is not None and seg_per_launch) else None,
         "fp32_flops_per_segment": flops32 / seg_per_launch if (flops32 is not None and seg_per_launch) else None,
         "valu_lane_util": per["SQ_THREAD_CYCLES_VALU"] / (64 * act)

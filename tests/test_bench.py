@@ -74,7 +74,8 @@ def test_pmc_record_must_match_kernel_build_and_workload(bench, monkeypatch, tmp
     assert abs(cw["frac"] - round(1000.0 / 2457.6, 4)) < 1e-9 and r3["valu"]["lane_util"] == 0.5
     assert abs(r3["valu"]["useful_frac"] - round(1000.0 / 2457.6 * 0.5, 4)) < 1e-9
     fl = r3["valu"]["fp64_flops"]
-    assert abs(fl["achieved"] - 400.0 * 1e9 / 0.05 / 1e12) < 1e-9 and fl["peak"] == 78.6
+    assert abs(fl["issued"] - 400.0 * 1e9 / 0.05 / 1e12) < 1e-9 and fl["peak"] == 78.6
+    assert abs(fl["achieved"] - 0.5 * 400.0 * 1e9 / 0.05 / 1e12) < 1e-9
     assert r3["write_bytes"] == 5e8
     r2 = bench.roofline(a, rec["kernel"], "stale", seg=2e9, ms=100.0, launches=2, algo=68 * 2e9)
     assert r2["bound"] == "hbm" and r2["traffic"] is None and "no PMC record" in r2["pmc"] and "valu" not in r2
@@ -102,7 +103,7 @@ def test_pmc_derivation_is_bounded(monkeypatch):
     other = 1000.0 - 50.0 * len(b.VALU_COST)
     want = (sum(50.0 * c for c in b.VALU_COST.values()) + b.VALU_COST_OTHER * other) / 64 / 10
     assert abs(d["valu_class_cycles_per_segment"] - want) < 1e-9
-    assert d["fp64_flops_per_segment"] == 6464.0 / 640.0 and d["valu_lane_util"] == 0.5
+    assert d["fp64_flops_per_segment"] == 6400.0 * 64 / 640.0 and d["valu_lane_util"] == 0.5
     assert d["hbm_bytes_per_launch"] == 2048 + 2048
     del per["SQ_INSTS_VALU_CVT"]
     assert p.derive(per, 640.0)["valu_class_cycles_per_segment"] is None
