@@ -284,7 +284,11 @@ struct scene {
 // F_NOLIGHTS: the scene has no lights, so the mixture-pdf branch of the
 // lambertian bounce is compiled out instead.
 enum : int { F_MEDIA = 1, F_WBVH = 2, F_GBVH = 4, F_YSPH = 8, F_STATIC = 16, F_LIGHTS = 32, F_BLACK = 64,
-             F_NOLIGHTS = 128 };
+             F_NOLIGHTS = 128,
+             // every camera ray of the render starts at the camera's origin (a
+             // pinhole camera, lens_radius 0, whose origin has no zero
+             // coordinate: origin + offset is then exactly origin, camera.h:48)
+             F_PIN = 256 };
 
 // Uniform scene reads.  The scene is read-only for a whole launch; reading
 // it through the constant address space lets the compiler use scalar loads
@@ -1557,10 +1561,45 @@ RTW_D bool boundary_t(const scene& S, const entry_v& e, const ray& r, double t0,
 template <int F, class STK>
 RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_min, double t_max, uint32_t& rng,
                     double& t_out, STK& stk) {
-    const ray r = ops_in<true>(e, rw, 0, rd<true>(&e.p->n_outer_ops));
+    const int n_outer = rd<true>(&e.p->n_outer_ops);
+    const ray r = ops_in<true>(e, rw, 0, n_outer);
     double t1, t2;
-    if (!boundary_t<F>(S, e, r, -kDblMax, kDblMax, t1, stk)) return false;
-    if (!boundary_t<F>(S, e, r, t1 + kStep, kDblMax, t2, stk)) return false;
+#ifndef RTW_MEDIUM_ONE_QUADRATIC
+#define RTW_MEDIUM_ONE_QUADRATIC 1
+#endif
+    if (RTW_MEDIUM_ONE_QUADRATIC && e.n_prims == 1 && e.bvh_root < 0 && is_sphere(ld(&S.prims[e.first_prim].type))) {
+        // A boundary that is one sphere (wave-uniform: the media walk's
+        // entries are): both probes (hittable.h:438-449) are that sphere's
+        // test on the same ray, so its quadratic is solved once and each
+        // probe applies its own range to the two roots, as group_scan would
+        // (near root if in (t_lo, DBL_MAX), else the far one).
+        const ray lr = ops_in<true>(e, r, n_outer, e.n_ops);
+        const rtw_prim q = uprim(S.prims, e.first_prim);
+        const d3 oc = lr.o - sphere_center(q, lr.t, motion_frac(S, lr.t, e.movers));
+        const double a = dot(lr.d, lr.d);
+        const double b = dot(oc, lr.d);
+        const double c = dot(oc, oc) - q.p[9];
+        const double disc = b * b - a * c;
+        if (!(disc > 0)) return false;
+        const double sq = __builtin_sqrt(disc);
+        const double r0 = (-b - sq) / a, r1 = (-b + sq) / a;
+        if (r0 < kDblMax && r0 > -kDblMax)
+            t1 = r0;
+        else if (r1 < kDblMax && r1 > -kDblMax)
+            t1 = r1;
+        else
+            return false;
+        const double lo = t1 + kStep;
+        if (r0 < kDblMax && r0 > lo)
+            t2 = r0;
+        else if (r1 < kDblMax && r1 > lo)
+            t2 = r1;
+        else
+            return false;
+    } else {
+        if (!boundary_t<F>(S, e, r, -kDblMax, kDblMax, t1, stk)) return false;
+        if (!boundary_t<F>(S, e, r, t1 + kStep, kDblMax, t2, stk)) return false;
+    }
     if (t1 < t_min) t1 = t_min;
     if (t2 > t_max) t2 = t_max;
     if (t1 >= t2) return false;

@@ -656,11 +656,32 @@ __global__ __launch_bounds__(kBlock) RTW_SEG_ATTR void k_segment(scene S, job_t 
 #ifndef RTW_PBATCH
 #define RTW_PBATCH(F) 64
 #endif
-template <int NB>
+// PIN (F_PIN): the origins are the camera's, read from the camera where a
+// sample is popped instead of stored per entry -- 24 B x 64 per wave less LDS
+// (24 KB per 1 024-thread workgroup), which the BVH node packet takes.
+template <int NB, bool PIN = false>
 struct ray_batch_t {  // one wave's buffer of generated camera samples (LDS)
-    double ox[NB], oy[NB], oz[NB], dx[NB], dy[NB], dz[NB], tm[NB];
+    double ox[PIN ? 1 : NB], oy[PIN ? 1 : NB], oz[PIN ? 1 : NB];
+    double dx[NB], dy[NB], dz[NB], tm[NB];
     uint32_t rng[NB], q[NB];
 };
+
+// the camera's origin (F_PIN batches), scalar loads through an opaque
+// pointer as in camera_sample
+__device__ __forceinline__ d3 camera_origin(const job_t& J) {
+    const rtw_camera_desc* cp = J.cam;
+    asm volatile("" : "+s"(cp));
+    return d3{ld(&cp->origin[0]), ld(&cp->origin[1]), ld(&cp->origin[2])};
+}
+// F_PIN applies to a render whose camera makes every ray at its origin
+// (-DRTW_PIN_KERNELS=0: never, for A/B)
+#ifndef RTW_PIN_KERNELS
+#define RTW_PIN_KERNELS 1
+#endif
+inline bool camera_is_pinhole(const rtw_camera_desc& c) {
+    return RTW_PIN_KERNELS && c.lens_radius == 0.0 && c.origin[0] != 0.0 && c.origin[1] != 0.0 &&
+           c.origin[2] != 0.0;
+}
 
 // Occupancy: left alone the compiler gives k_persist 160-230 VGPRs (2-3
 // waves per SIMD).  Capping at 128 (4 waves) costs some spilled registers and
@@ -742,10 +763,11 @@ void k_persist(persist_args) {
     constexpr bool BIN = RTW_BIN_RAYS(F) && !DIRECT;
     constexpr bool PARK = RTW_PARK_ORIGIN(F) && !DIRECT && !BIN;
     constexpr int NB = DIRECT ? 1 : RTW_PBATCH(F);
+    constexpr bool PIN = (F & F_PIN) != 0;
     static_assert(NB >= 1 && NB <= 64, "batch of one wave");
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kPWaves];
-    __shared__ ray_batch_t<NB> s_batch[DIRECT ? 1 : kPWaves];
+    __shared__ ray_batch_t<NB, PIN> s_batch[DIRECT ? 1 : kPWaves];
     // DIRECT: each lane's ray (o, d, time); PARK: its origin
     __shared__ double s_ray[DIRECT ? 7 : (PARK ? 3 : 1)][kPBlock];
     __shared__ double s_thr[3][kPBlock];  // each lane's path throughput
@@ -833,7 +855,7 @@ void k_persist(persist_args) {
         } else {
             // (the wave's batch too: formed once per kernel, its per-array
             // addresses were held in 15 VGPRs across the whole loop)
-            ray_batch_t<NB>& B = s_batch[tid >> 6];
+            ray_batch_t<NB, PIN>& B = s_batch[tid >> 6];
             for (int round = 0; round < 2; ++round) {
                 const unsigned long long m = __ballot(x.depth == 0);
                 if (!m) break;
@@ -868,7 +890,7 @@ void k_persist(persist_args) {
                     if (got) {  // (lanes >= NB get no id)
                         uint32_t rng;
                         const ray r = camera_sample(J, q, rng);
-                        B.ox[ln] = r.o.x, B.oy[ln] = r.o.y, B.oz[ln] = r.o.z;
+                        if constexpr (!PIN) B.ox[ln] = r.o.x, B.oy[ln] = r.o.y, B.oz[ln] = r.o.z;
                         B.dx[ln] = r.d.x, B.dy[ln] = r.d.y, B.dz[ln] = r.d.z;
                         B.tm[ln] = r.t;
                         B.rng[ln] = rng;
@@ -883,7 +905,8 @@ void k_persist(persist_args) {
                 const uint32_t avail = bh - bl;
                 if (x.depth == 0 && rank < avail) {
                     const uint32_t k = bl + rank;
-                    x.r = ray{d3{B.ox[k], B.oy[k], B.oz[k]}, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
+                    const d3 o = PIN ? camera_origin(args_now().J) : d3{B.ox[k], B.oy[k], B.oz[k]};
+                    x.r = ray{o, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
                     if constexpr (PARK) s_ray[0][tid] = x.r.o.x, s_ray[1][tid] = x.r.o.y, s_ray[2][tid] = x.r.o.z;
                     x.rng = B.rng[k];
                     const uint32_t hm = BIN ? home : tid;
@@ -1877,6 +1900,7 @@ struct handle_t {
     // BVH boxes of moving spheres cover the desc camera's shutter only
     bool bvh_motion = false;
     double shutter0 = 0.0, shutter1 = 0.0;
+    bool desc_pin = false;  // the desc's own camera is a pinhole (F_PIN kernels; rtw_scene_query)
     std::vector<hipEvent_t> events;
 };
 
@@ -2445,6 +2469,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     }
     bool movers = false;
     for (int k = 0; k < d->n_prims; ++k) movers |= d->prims[k].type == RTW_PRIM_MOVING_SPHERE;
+    h->desc_pin = camera_is_pinhole(d->camera);
     h->bvh_motion = movers && d->n_bvh_nodes > 0;
     h->shutter0 = std::min(d->camera.time0, d->camera.time1);
     h->shutter1 = std::max(d->camera.time0, d->camera.time1);
@@ -2741,13 +2766,28 @@ void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t s
 
 bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const scene& S, const job_t& J, ctrs_t* C,
                     const char* base, uint32_t bytes, int stack_need = kStack, bool ysph = false,
-                    bool static_scene = false, bool lights = false, bool black = false, std::string* name = nullptr) {
+                    bool static_scene = false, bool lights = false, bool black = false, bool pin = false,
+                    std::string* name = nullptr) {
     if (ysph && !(f & (F_WBVH | F_MEDIA))) f |= F_YSPH;  // world runs are walked: y-sphere scans
     const int pick = pick_shade_mask(mask);
     // specialised kernels only
     const int fs = f | (static_scene ? F_STATIC : 0) | (lights ? F_LIGHTS : F_NOLIGHTS) | (black ? F_BLACK : 0);
     const bool lds = bytes <= kShadeLdsMax;
     const size_t shm = lds ? bytes : 0;
+    // the BVH kernels' pinhole forms (F_PIN: camera batches without
+    // origins, a larger node packet) for renders whose camera allows it
+    if (pin) {
+#define RTW_PIN(FF, MM, LL)                                                                    \
+        if ((fs | F_PIN) == (FF) && pick == (MM) && lds == (LL)) {                             \
+            launch_pk<FF, MM, LL>(probe, name, cus, shm, st, S, J, C, base, bytes, stack_need); \
+            return true;                                                                       \
+        }
+#ifndef RTW_SUBSET
+        RTW_PIN(F_WBVH | F_NOLIGHTS | F_PIN, SF_METAL | SF_DIEL, false)
+        RTW_PIN(F_MEDIA | F_GBVH | F_LIGHTS | F_BLACK | F_PIN, SF_NOCHECKER, false)
+#endif
+#undef RTW_PIN
+    }
 #define RTW_PER(FF, MM, LL)                                                                     \
     if ((f == (FF) || fs == (FF)) && pick == (MM) && lds == (LL)) {                           \
         launch_pk<FF, MM, LL>(probe, name, cus, shm, st, S, J, C, base, bytes, stack_need);   \
@@ -2961,7 +3001,7 @@ std::string render_kernel_name(const handle_t* h) {
     if (!wavefront && launch_persist(true, h->features, h->shade_mask, 0, nullptr, h->S, J, nullptr, h->scene_base,
                                      h->shade_bytes, lst_stack_need(h), h->ysph, !h->movers, h->S.n_lights > 0,
                                      h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL,
-                                     &name))
+                                     h->desc_pin, &name))
         return name;
     const char* split_env = std::getenv("RTW_SPLIT");
     const paths_t A{};
@@ -3252,12 +3292,14 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         FA.cam.time0 = (float)c.time0, FA.cam.dtime = (float)(c.time1 - c.time0);
         FA.cam.lens_radius = (float)c.lens_radius;
     }
+    const bool pin = camera_is_pinhole(*camera);
     const bool persistent = fast || (!(mode_env && std::string(mode_env) == "wavefront") &&
                                      launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J, C,
                                                     h->scene_base, h->shade_bytes, lst_stack_need(h), h->ysph, !h->movers,
                                                     h->S.n_lights > 0,
                                                     h->S.background != RTW_BG_GRADIENT &&
-                                                        h->S.render_type != RTW_RENDER_NORMAL));
+                                                        h->S.render_type != RTW_RENDER_NORMAL,
+                                                    pin));
 
     for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
@@ -3279,7 +3321,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
             } else {
                 launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base,
                                h->shade_bytes, lst_stack_need(h), h->ysph, !h->movers, h->S.n_lights > 0,
-                               h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL);
+                               h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL, pin);
             }
             HIPCHK(hipGetLastError());
             if (timed) {
