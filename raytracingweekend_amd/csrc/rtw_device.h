@@ -987,8 +987,43 @@ RTW_D void rect_arbitrate_far(const scene& S, int pi, const ray& r, double t_min
 #ifndef RTW_BOX_NEAR
 #define RTW_BOX_NEAR 0
 #endif
+// A box's six rect tests divide by only three values, d.x, d.y and d.z
+// (each face pair shares its plane axis), so a box computes the three
+// reciprocals once (rtw_div.h rcp_hw) and each face's t = (k - o.K) / d.K
+// costs a multiply and two fma (div_hw) instead of a full division --
+// bit-identical under make_rect_rcp's conditions (scene::fast_div, |o| <=
+// 2^40, |d.K| in [2^-200, 2^200]) when t_min >= 0.001 (a numerator below
+// 2^-800 then gives quotients that t_min rejects alike); other lanes, and
+// boxes probed as a medium's boundary (t_min = -DBL_MAX), divide exactly.
+#ifndef RTW_BOX_RCP
+#define RTW_BOX_RCP 1
+#endif
+template <int K, int A, int B>
+RTW_D void rect_arbitrate_rcp(const scene& S, int pi, const ray& r, const rect_rcp& rr, double t_min, hit_state& h) {
+    double t;
+    const rtw_prim& q = S.prims[pi];  // fields read where the test uses them
+    if (!rect_axis_rcp<K, A, B>(q, r, rr, t_min, h.t, t)) return;
+    if (better(t, pi, true, h.t, h.prim, h.rect, h.prim != -1)) {
+        h.t = t;
+        h.prim = pi;
+        h.rect = true;
+    }
+}
 template <bool U = false>
 RTW_D void box_arbitrate(const scene& S, int first, const ray& r, double t_min, hit_state& h) {
+    if constexpr (RTW_BOX_RCP && !RTW_BOX_NEAR && !U) {
+        rect_rcp rr = make_rect_rcp(S, r);
+        const bool tmin_ok = t_min >= kTMin;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rr.ok[k] = rr.ok[k] && tmin_ok;
+        rect_arbitrate_rcp<2, 0, 1>(S, first, r, rr, t_min, h);
+        rect_arbitrate_rcp<2, 0, 1>(S, first + 1, r, rr, t_min, h);
+        rect_arbitrate_rcp<1, 0, 2>(S, first + 2, r, rr, t_min, h);
+        rect_arbitrate_rcp<1, 0, 2>(S, first + 3, r, rr, t_min, h);
+        rect_arbitrate_rcp<0, 1, 2>(S, first + 4, r, rr, t_min, h);
+        rect_arbitrate_rcp<0, 1, 2>(S, first + 5, r, rr, t_min, h);
+        return;
+    }
     if constexpr (RTW_BOX_NEAR && !U) {
         const int nz = first + (r.d.z > 0), ny = first + 2 + (r.d.y > 0), nx = first + 4 + (r.d.x > 0);
         const int pair = 2 * first + 1;  // (first + 2j) + (first + 2j + 1) - 4j
