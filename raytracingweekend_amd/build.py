@@ -73,6 +73,15 @@ def _run(cmd):
     return r
 
 
+def _link(objs, out: Path) -> None:
+    """Link into a temporary file and rename it over `out` (atomic: a
+    snapshot of the tree taken meanwhile sees the old library or the new
+    one, never a half-written file)."""
+    tmp = out.with_name(out.name + ".tmp")
+    _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), *LIBS, "-o", str(tmp)])
+    os.replace(tmp, out)
+
+
 def _compile(src: Path, force: bool, extra=(), tag: str = "") -> Path:
     obj = BUILD / (src.name + tag + ".o")
     deps = DEVICE_HEADERS if src.suffix == ".hip" else HEADERS
@@ -92,7 +101,7 @@ def build_library(force: bool = False) -> Path:
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
     if force or _newer(LIB, objs):
-        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), *LIBS, "-o", str(LIB)])
+        _link(objs, LIB)
     return LIB
 
 
@@ -106,7 +115,7 @@ def build_variant_library(name: str, defines, force: bool = False, host: bool = 
     objs = [_compile(s, force, flags, f".{name}") for s in DEVICE_SOURCES]
     objs += [_compile(s, force, flags, f".{name}") if host else _compile(s, force) for s in HOST_SOURCES]
     if force or _newer(out, objs):
-        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), *LIBS, "-o", str(out)])
+        _link(objs, out)
     return out
 
 
@@ -119,7 +128,7 @@ def build_profiling_library(force: bool = False) -> Path:
     objs = [_compile(s, force, ["-DRTW_PROF"], ".prof") for s in DEVICE_SOURCES]
     objs += [_compile(s, force) for s in HOST_SOURCES]
     if force or _newer(out, objs):
-        _run([HIPCC, *DEVICE, "-shared", "-fPIC", *map(str, objs), *LIBS, "-o", str(out)])
+        _link(objs, out)
     return out
 
 

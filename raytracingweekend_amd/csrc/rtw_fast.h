@@ -275,7 +275,11 @@ RTW_D void ysphere_scan(const fscene& S, int first, int n, const fray& r, float 
         float t;
         if (sphere_t(q, r, tmin, h.t, t)) h.t = t, h.prim = first + i, h.rect = false;
     };
-    const f2 ox2 = r.o.x, oy2 = r.o.y, oz2 = r.o.z, dx2 = r.d.x, dy2 = r.d.y, dz2 = r.d.z, fc2 = fc, a2 = a;
+    // the ray's components splatted into pairs from register copies (built
+    // from the struct itself, the compiler kept the caller's ray in scratch)
+    float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    asm volatile("" : "+v"(ox), "+v"(oy), "+v"(oz), "+v"(dx), "+v"(dy), "+v"(dz));
+    const f2 ox2 = ox, oy2 = oy, oz2 = oz, dx2 = dx, dy2 = dy, dz2 = dz, fc2 = fc, a2 = a;
     auto disc = [&](f2 cx, f2 cy, f2 cz, f2 dy, f2 rr, f2& slack) {
         const f2 ocx = ox2 - cx, ocz = oz2 - cz;
         const f2 ocy = __builtin_elementwise_fma(-dy, fc2, oy2 - cy);
@@ -548,16 +552,19 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 ysphere_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), r, kTMinF, h, fc);
                 continue;
             }
-            fray lr = r;
+            // (two scan sites rather than one over a conditionally
+            // transformed copy of the ray: that copy was kept in scratch)
             if (ei >= 0) {
                 const ent_v e = view_entry<true>(S, ei);
-                lr = ops_in<true>(e, r, 0, e.n_ops);
+                const fray lr = ops_in<true>(e, r, 0, e.n_ops);
                 if ((F & rtwd::F_GBVH) && e.bvh_root >= 0) {
                     group_bvh(S, e.bvh_root, lr, kTMinF, h, stk, 0);
                     continue;
                 }
+                group_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), lr, kTMinF, h);
+            } else {
+                group_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), r, kTMinF, h);
             }
-            group_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), lr, kTMinF, h);
         }
     }
     return h;
@@ -593,7 +600,7 @@ RTW_D void hit_record(const fscene& S, const fray& r, const fhit& h, f3& p, f3& 
 }
 
 // ------------------------------------------------------------------ textures
-RTW_D float perlin_noise(const fscene& S, f3 p) {  // noise.h:89-151
+RTW_D float perlin_noise(const float* ranvec, const int32_t* perm, f3 p) {  // noise.h:89-151
     const float fx = __builtin_floorf(p.x), fy = __builtin_floorf(p.y), fz = __builtin_floorf(p.z);
     const float u = p.x - fx, v = p.y - fy, w = p.z - fz;
     const int i = (int)fx, j = (int)fy, k = (int)fz;
@@ -605,21 +612,27 @@ RTW_D float perlin_noise(const fscene& S, f3 p) {  // noise.h:89-151
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                const int idx = S.perm[(i + a) & 255] ^ S.perm[256 + ((j + b) & 255)] ^ S.perm[512 + ((k + c) & 255)];
-                const f3 g = ldf3(S.ranvec + 3 * idx);
+                const int idx = perm[(i + a) & 255] ^ perm[256 + ((j + b) & 255)] ^ perm[512 + ((k + c) & 255)];
+                const f3 g = ldf3(ranvec + 3 * idx);
                 accum += (a ? uu : 1 - uu) * (b ? vv : 1 - vv) * (c ? ww : 1 - ww) * dot(g, f3{u - a, v - b, w - c});
             }
     return accum;
 }
-RTW_D float turb(const fscene& S, f3 p) {  // noise.h:74-86
+RTW_D float turb(const float* ranvec, const int32_t* perm, f3 p) {  // noise.h:74-86
     float accum = 0, weight = 1.0f;
     for (int i = 0; i < 7; ++i) {
-        accum += weight * perlin_noise(S, p);
+        accum += weight * perlin_noise(ranvec, perm, p);
         weight *= 0.5f;
         p = p * 2.0f;
     }
     return __builtin_fabsf(accum);
 }
+// NOISE = false: the scene has no noise texture (kernels for such scenes
+// compile the marble branch out: its seven octaves of eight gradients are
+// the widest register peak of the fp32 kernels, and inlined they set the
+// register budget of every path -- the list kernel spilled in shading for it
+// though Cornell has no noise texture)
+template <bool NOISE = true>
 RTW_D f3 texture_value(const fscene& S, int id, f3 p) {
     for (int guard = 0; guard < 8; ++guard) {
         const tex32& t = S.textures[id];
@@ -629,7 +642,8 @@ RTW_D f3 texture_value(const fscene& S, int id, f3 p) {
             id = sines < 0 ? t.odd : t.even;
             continue;
         }
-        const float v = 0.5f * (1 + sinf(t.scale * p.z + 10 * turb(S, p)));  // texture.h:57-68
+        if constexpr (!NOISE) return f3{0, 0, 0};  // unreachable: no noise texture in the scene
+        const float v = 0.5f * (1 + sinf(t.scale * p.z + 10 * turb(S.ranvec, S.perm, p)));  // texture.h:57-68
         return f3{v, v, v};
     }
     return f3{0, 0, 0};
@@ -725,6 +739,7 @@ struct seg_f {
     f3 w;
     fray next;
 };
+template <bool NOISE = true>
 RTW_D seg_f shade(const fscene& S, const fray& r, const fhit& h, uint32_t& rng, uint32_t depth) {
     seg_f o{false, f3{0, 0, 0}, r};
     if (h.prim == -1) {  // background :141-159
@@ -741,17 +756,28 @@ RTW_D seg_f shade(const fscene& S, const fray& r, const fhit& h, uint32_t& rng, 
         o.w = (n + f3{1, 1, 1}) * 0.5f;
         return o;
     }
-    const mat32& M = S.materials[mat];
-    const int type = M.type;
+    // The material's type and texture are read here; its other fields where
+    // a branch uses them, through an opaque copy of the index (a material
+    // pointer formed once was held in a VGPR pair across every branch, and
+    // spilled to scratch: most of the fp32 kernels' write traffic).
+    const int type = S.materials[mat].type;
+    const int tex = S.materials[mat].texture;
+    auto mat_now = [&]() -> const mat32& {
+        int m = mat;
+        asm volatile("" : "+v"(m));
+        return S.materials[m];
+    };
     if (type == RTW_MAT_DIFFUSE_LIGHT) {  // material.h:232-244, one-sided
-        if (dot(n, r.d) > 0) o.w = texture_value(S, M.texture, p);
+        if (dot(n, r.d) > 0) o.w = texture_value<NOISE>(S, tex, p);
         return o;
     }
     f3 f{1, 1, 1}, dir;
     if (type == RTW_MAT_METAL) {  // material.h:128-136
+        const mat32& M = mat_now();
         dir = reflect(normalize(r.d), n) + random_in_unit_sphere(rng) * M.fuzz;
         f = ldf3(M.albedo);
     } else if (type == RTW_MAT_DIELECTRIC) {  // material.h:146-222
+        const mat32& M = mat_now();
         const float dn = dot(r.d, n), il = __builtin_amdgcn_rsqf(len2(r.d));
         const float ri = M.ref_idx;
         f3 outward;
@@ -779,7 +805,7 @@ RTW_D seg_f shade(const fscene& S, const fray& r, const fhit& h, uint32_t& rng, 
         dir = u01(rng) < reflect_prob ? reflect(r.d, n) : refracted;
     } else if (type == RTW_MAT_ISOTROPIC) {  // material.h:257-262
         dir = random_in_unit_sphere(rng);
-        f = texture_value(S, M.texture, p);
+        f = texture_value<NOISE>(S, tex, p);
     } else {  // lambertian material.h:81-119 + RayTracingWeekend.cpp:112-132
         const onbf fr = frame(S, n, fp);
         float pdf_val;
@@ -796,7 +822,7 @@ RTW_D seg_f shade(const fscene& S, const fray& r, const fhit& h, uint32_t& rng, 
         if (!(pdf_val > 0)) return o;  // :126-127 returns emitted (0)
         const float cosine = dot(n, normalize(dir));
         const float spdf = cosine < 0 ? 0.0f : cosine * (1.0f / kPiF);
-        f = texture_value(S, M.texture, p) * (spdf * rcp(pdf_val));
+        f = texture_value<NOISE>(S, tex, p) * (spdf * rcp(pdf_val));
     }
     if (depth <= 1) return o;  // the next color() call has depth 0: returns 0
     o.cont = true;

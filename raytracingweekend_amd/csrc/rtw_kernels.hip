@@ -1295,6 +1295,19 @@ void k_persist_sort(persist_args) {
 // id -- and camera samples taken by idle lanes (one queue reservation per
 // wave).  Waves run independently (no block barrier in the loop), so a wave
 // leaves as soon as the queue is dry and its last path has ended.
+// The fast mode's per-sample radiance record: 12 B of fp32 (k_reduce<float>
+// sums it in double in sample order, as it sums fp64 records); 24 B of fp64
+// under RTW_PIXEL_MAJOR, whose staged reduce reads doubles only.
+__device__ __forceinline__ void store_record_f32(double* L, uint32_t q, float x, float y, float z) {
+#if RTW_PIXEL_MAJOR
+    double* o = L + 3 * (size_t)q;
+    o[0] = (double)x, o[1] = (double)y, o[2] = (double)z;
+#else
+    float* o = reinterpret_cast<float*>(L) + 3 * (size_t)q;
+    o[0] = x, o[1] = y, o[2] = z;
+#endif
+}
+
 struct fast_args {
     rtwf::fscene S;
     job_t J;
@@ -1312,6 +1325,10 @@ __device__ __forceinline__ const fast_args& fast_args_now() {
     return *(const fast_args*)p;
 }
 
+// fp32 kernels for scenes without a noise texture (F bit, fast kernels only):
+// the marble texture compiled out of shading (rtw_fast.h texture_value)
+constexpr int FF_NONOISE = 1 << 12;
+
 // Waves per SIMD of k_fast.  With the node packet, 8 waves in two
 // 1 024-thread workgroups per CU (each with a ~48 KB packet) beat 6 waves in
 // two 768-thread ones (~56 KB packets, no spills) although the kernel then
@@ -1326,6 +1343,7 @@ template <int F, bool LST>
 __global__ __launch_bounds__(rtwf::kFastBlock) __attribute__((amdgpu_waves_per_eu(RTW_FAST_BVH_WAVES)))
 void k_fast(fast_args) {
     using namespace rtwf;
+    constexpr bool NOISE = (F & FF_NONOISE) == 0;
     constexpr int kFW = kFastBlock / 64;
     extern __shared__ __attribute__((aligned(16))) char s_nodes[];
     __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kFastBlock];
@@ -1401,7 +1419,7 @@ void k_fast(fast_args) {
         }
         ++segs;
         // one segment of color() (RayTracingWeekend.cpp:52-159)
-        const seg_f sg = shade(fast_args_now().S, r, h, rng, depth);
+        const seg_f sg = shade<NOISE>(fast_args_now().S, r, h, rng, depth);
         bool end = !sg.cont;
         f3 L{0, 0, 0};
         if (sg.cont) {
@@ -1412,8 +1430,7 @@ void k_fast(fast_args) {
             L = thr * sg.w;
         }
         if (end) {
-            double* o = fast_args_now().J.L + 3 * (size_t)q;
-            o[0] = (double)L.x, o[1] = (double)L.y, o[2] = (double)L.z;
+            store_record_f32(fast_args_now().J.L, q, L.x, L.y, L.z);
             depth = 0;
         }
     }
@@ -1461,6 +1478,7 @@ template <int F, bool LDS>
 __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(RTW_FAST_WAVES)))
 void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
     using namespace rtwf;
+    constexpr bool NOISE = (F & FF_NONOISE) == 0;
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_kc[kSortWaves][FK_N];
     __shared__ uint32_t s_seg[kSortWaves];
@@ -1584,7 +1602,7 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
             const fray rr{f3{x_o[0][me], x_o[1][me], x_o[2][me]}, f3{x_d[0][me], x_d[1][me], x_d[2][me]}, x_tm[me]};
             const fhit hh{x_t[me], x_prim[me], false};
             const fast_args& A = fast_args_now();
-            const seg_f sg = shade(LDS ? lds_fscene(A.S, base, bytes, s_scene) : A.S, rr, hh, rng, depth);
+            const seg_f sg = shade<NOISE>(LDS ? lds_fscene(A.S, base, bytes, s_scene) : A.S, rr, hh, rng, depth);
             const uint32_t home = x_home[me];
             const f3 thr{s_thr[0][home], s_thr[1][home], s_thr[2][home]};
             if (sg.cont) {
@@ -1593,8 +1611,7 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
                 x_d[0][me] = sg.next.d.x, x_d[1][me] = sg.next.d.y, x_d[2][me] = sg.next.d.z;
                 --depth;
             } else {
-                double* o = A.J.L + 3 * (size_t)x_q[me];
-                o[0] = (double)(thr.x * sg.w.x), o[1] = (double)(thr.y * sg.w.y), o[2] = (double)(thr.z * sg.w.z);
+                store_record_f32(A.J.L, x_q[me], thr.x * sg.w.x, thr.y * sg.w.y, thr.z * sg.w.z);
                 depth = 0;
             }
         }
@@ -1786,15 +1803,19 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ L,
     }
 }
 #else
-__global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ L, uint32_t npix, uint32_t spp,
+// Records are doubles (fp64 mode) or floats (the fp32 fast mode's radiance
+// is single precision: 12 B records, converted exactly to double here and
+// summed in the same order, so its sums are unchanged).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_reduce(const T* __restrict__ L, uint32_t npix, uint32_t spp,
                                                    double* __restrict__ run) {
     for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < npix; p += gridDim.x * kBlock) {
         double r = run[3 * p], g = run[3 * p + 1], bl = run[3 * p + 2];
         for (uint32_t s = 0; s < spp; ++s) {
-            const double* x = L + 3 * ((size_t)s * npix + p);
-            r = r + x[0];
-            g = g + x[1];
-            bl = bl + x[2];
+            const T* x = L + 3 * ((size_t)s * npix + p);
+            r = r + (double)x[0];
+            g = g + (double)x[1];
+            bl = bl + (double)x[2];
         }
         run[3 * p] = r, run[3 * p + 1] = g, run[3 * p + 2] = bl;
     }
@@ -2893,10 +2914,18 @@ bool fast_sort_enabled() {
 int lst_stack_need(const handle_t* h) { return RTW_BVH4 ? h->stack4_need : h->stack_need; }
 void launch_fast(bool probe, const handle_t* h, hipStream_t st, const fast_args& A, std::string* name = nullptr) {
     const int f = h->features & (F_MEDIA | F_WBVH | F_GBVH);
+#ifdef RTW_SUBSET_FAST  // experiment builds (scripts/ru_kernel.sh): the list scenes' fp32 kernel only
+    launch_fast_sort_t<FF_NONOISE, true>(probe, name, h->cus, st, A, static_cast<const char*>(h->scene32.p),
+                                         h->f32_bytes);
+    launch_fast_t<F_WBVH | FF_NONOISE, true>(probe, name, h->cus, st, A);
+#else
     if ((f & (F_WBVH | F_GBVH)) == 0 && fast_sort_enabled()) {  // list scenes: regrouping kernel
         const char* base = static_cast<const char*>(h->scene32.p);
         const bool lds = h->f32_bytes <= kShadeLdsMax;
-        if (f == F_MEDIA)
+        if (f == 0 && !(h->shade_mask & SF_NOISE))  // Cornell, random_balls: no marble texture
+            lds ? launch_fast_sort_t<FF_NONOISE, true>(probe, name, h->cus, st, A, base, h->f32_bytes)
+                : launch_fast_sort_t<FF_NONOISE, false>(probe, name, h->cus, st, A, base, h->f32_bytes);
+        else if (f == F_MEDIA)
             lds ? launch_fast_sort_t<F_MEDIA, true>(probe, name, h->cus, st, A, base, h->f32_bytes)
                 : launch_fast_sort_t<F_MEDIA, false>(probe, name, h->cus, st, A, base, h->f32_bytes);
         else
@@ -2905,6 +2934,10 @@ void launch_fast(bool probe, const handle_t* h, hipStream_t st, const fast_args&
         return;
     }
     const bool lst = (f & (F_WBVH | F_GBVH)) && h->stack_need <= kLdsStack && h->S.n_nodes < 65536;
+    if (f == F_WBVH && lst && !(h->shade_mask & SF_NOISE)) {  // random_balls + BVH: no marble texture
+        launch_fast_t<F_WBVH | FF_NONOISE, true>(probe, name, h->cus, st, A);
+        return;
+    }
     switch (f * 2 + (lst ? 1 : 0)) {
 #define RTW_FAST(FF, LL) \
     case (FF) * 2 + (LL ? 1 : 0): launch_fast_t<FF, LL>(probe, name, h->cus, st, A); break;
@@ -2922,6 +2955,7 @@ void launch_fast(bool probe, const handle_t* h, hipStream_t st, const fast_args&
     default:
         launch_fast_t<F_MEDIA | F_GBVH, false>(probe, name, h->cus, st, A);
     }
+#endif
 }
 
 void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_t& J, const paths_t& A,
@@ -3330,8 +3364,17 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
             }
             stats.launches_intersect++;
             stats.iterations++;
+#if RTW_PIXEL_MAJOR
             hipLaunchKernelGGL(k_reduce, dim3(reduce_grid(npix)), dim3(kBlock), 0,
                                st, J.L, (uint32_t)npix, S_pass, run);
+#else
+            if (fast)
+                hipLaunchKernelGGL(k_reduce<float>, dim3(reduce_grid(npix)), dim3(kBlock), 0, st,
+                                   reinterpret_cast<const float*>(J.L), (uint32_t)npix, S_pass, run);
+            else
+                hipLaunchKernelGGL(k_reduce<double>, dim3(reduce_grid(npix)), dim3(kBlock), 0, st, J.L,
+                                   (uint32_t)npix, S_pass, run);
+#endif
             HIPCHK(hipGetLastError());
             stats.samples += J.total;
             continue;
@@ -3410,8 +3453,13 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 if (tail && snap.n == 0) break;
             }
         }
+#if RTW_PIXEL_MAJOR
         hipLaunchKernelGGL(k_reduce, dim3(reduce_grid(npix)), dim3(kBlock), 0, st,
                            J.L, (uint32_t)npix, S_pass, run);
+#else
+        hipLaunchKernelGGL(k_reduce<double>, dim3(reduce_grid(npix)), dim3(kBlock), 0, st,
+                           J.L, (uint32_t)npix, S_pass, run);  // the wavefront form is fp64 only
+#endif
         HIPCHK(hipGetLastError());
         stats.samples += J.total;
     }
