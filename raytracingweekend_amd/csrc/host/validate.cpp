@@ -14,6 +14,8 @@ int validate_desc(const rtw_scene_desc* d) {
     if (d->n_entries < 0 || d->n_prims < 0 || d->n_materials < 0 || d->n_textures < 0 || d->n_lights < 0 ||
         d->n_bvh_nodes < 0 || d->n_bvh_items < 0 || d->n_visits < 0)
         return rtw_fail(RTW_ERR_INVALID, "negative array size in scene desc");
+    if (d->n_entries > (1 << 20) - 1)  // the media walk packs entry indices in 20 bits (rtw_device.h)
+        return rtw_fail(RTW_ERR_UNSUPPORTED, "more than 2^20 - 1 entries in scene desc");
     if ((d->n_entries && !d->entries) || (d->n_prims && !d->prims) || (d->n_materials && !d->materials) ||
         (d->n_textures && !d->textures) || (d->n_lights && !d->lights) || (d->n_bvh_nodes && !d->bvh_nodes) ||
         (d->n_bvh_items && !d->bvh_items) || (d->n_visits && !d->visits) ||

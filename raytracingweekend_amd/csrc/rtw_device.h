@@ -222,6 +222,14 @@ struct dev_op {
     int32_t type, pad;
     double p[3];
 };
+// The media walk (scene::media) lists entries in visit order; a visit of a
+// medium visited twice also names a boundary cache slot (1-based, bits
+// 20-23) and, on its later visit, kVisitReuse: the boundary distances depend
+// only on the ray and the medium, so the second list walk reuses the first's.
+constexpr int kMediumSlots = 4;
+constexpr int32_t kVisitSlotShift = 20;
+constexpr int32_t kVisitEntry = (1 << kVisitSlotShift) - 1;
+constexpr int32_t kVisitReuse = 1 << 24;
 struct scene {
     const rtw_prim* prims;
     const dev_entry* entries;
@@ -1009,13 +1017,27 @@ RTW_D void rect_arbitrate_rcp(const scene& S, int pi, const ray& r, const rect_r
         h.rect = true;
     }
 }
+// the six faces with the reciprocals of a leaf (leaf_items)
+RTW_D void box_arbitrate_rr(const scene& S, int first, const ray& r, const rect_rcp& rr, double t_min, hit_state& h) {
+    rect_arbitrate_rcp<2, 0, 1>(S, first, r, rr, t_min, h);
+    rect_arbitrate_rcp<2, 0, 1>(S, first + 1, r, rr, t_min, h);
+    rect_arbitrate_rcp<1, 0, 2>(S, first + 2, r, rr, t_min, h);
+    rect_arbitrate_rcp<1, 0, 2>(S, first + 3, r, rr, t_min, h);
+    rect_arbitrate_rcp<0, 1, 2>(S, first + 4, r, rr, t_min, h);
+    rect_arbitrate_rcp<0, 1, 2>(S, first + 5, r, rr, t_min, h);
+}
+// make_rect_rcp with the quotient rule's t_min condition folded in
+RTW_D rect_rcp make_rect_rcp_t(const scene& S, const ray& r, double t_min) {
+    rect_rcp rr = make_rect_rcp(S, r);
+    const bool tmin_ok = t_min >= kTMin;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) rr.ok[k] = rr.ok[k] && tmin_ok;
+    return rr;
+}
 template <bool U = false>
 RTW_D void box_arbitrate(const scene& S, int first, const ray& r, double t_min, hit_state& h) {
     if constexpr (RTW_BOX_RCP && !RTW_BOX_NEAR && !U) {
-        rect_rcp rr = make_rect_rcp(S, r);
-        const bool tmin_ok = t_min >= kTMin;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) rr.ok[k] = rr.ok[k] && tmin_ok;
+        const rect_rcp rr = make_rect_rcp_t(S, r, t_min);
         rect_arbitrate_rcp<2, 0, 1>(S, first, r, rr, t_min, h);
         rect_arbitrate_rcp<2, 0, 1>(S, first + 1, r, rr, t_min, h);
         rect_arbitrate_rcp<1, 0, 2>(S, first + 2, r, rr, t_min, h);
@@ -1086,6 +1108,44 @@ RTW_D void arbitrate_a(const scene& S, int pi, const ray& r, double t_min, hit_s
         h.t = t;
         h.prim = pi;
         h.rect = rl;
+    }
+}
+
+// The items of a group-BVH leaf, with reciprocals shared across the leaf:
+// the three of the ray's direction for its boxes' faces (box_arbitrate's rule)
+// and 1 / dot(d, d) for its spheres' roots (arbitrate_a's), each computed
+// only when one of the wave's leaves holds such an item.  Quotients are
+// bit-identical under the rules of make_rect_rcp / walk_quot with t_min >=
+// 0.001; other lanes (and boundary probes) divide exactly.
+#ifndef RTW_LEAF_RCP
+#define RTW_LEAF_RCP 1
+#endif
+RTW_D void leaf_items(const scene& S, int la, int lc, const ray& r, double t_min, hit_state& h, double fc) {
+    if constexpr (!RTW_LEAF_RCP || RTW_BOX_NEAR) {
+        for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
+        return;
+    }
+    bool box = false, sph = false;
+    for (int k = 0; k < lc; ++k) {
+        const int it = S.items[la + k];
+        box = box || (it & RTW_ITEM_BOX);
+        sph = sph || !(it & RTW_ITEM_BOX);
+    }
+    rect_rcp rr{};
+    double ya = 0.0;
+    bool oka = false;
+    if (box) rr = make_rect_rcp_t(S, r, t_min);
+    if (sph) {
+        const double a = dot(r.d, r.d);
+        ya = rcp_hw(a);
+        oka = t_min >= kTMin && walk_ray_ok(S, r, fc) && div_hw_ok_b(a);
+    }
+    for (int k = 0; k < lc; ++k) {
+        const int it = S.items[la + k];
+        if (it & RTW_ITEM_BOX)
+            box_arbitrate_rr(S, it & RTW_ITEM_INDEX, r, rr, t_min, h);
+        else
+            arbitrate_a(S, it, r, t_min, h, fc, ya, oka);
     }
 }
 
@@ -1550,7 +1610,7 @@ RTW_D void group_bvh(const scene& S, int root, int root4, const ray& r, double t
             if (lc == 0 && sp + 2 <= STK::cap) push_children(nd, dneg, stk, sp);
         }
         if (lc == 0) break;
-        for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
+        leaf_items(S, la, lc, r, t_min, h, fc);
     }
 #endif
 #else
@@ -1590,18 +1650,19 @@ RTW_D bool boundary_t(const scene& S, const entry_v& e, const ray& r, double t0,
     return true;
 }
 
-// constant_medium::hit hittable.h:430-479 (at most one draw per call), in
-// the frame of the transforms enclosing the medium (translate / rotate_y
-// hand it their moved ray, hittable.h:299-311, 373-404)
-template <int F, class STK>
-RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_min, double t_max, uint32_t& rng,
-                    double& t_out, STK& stk) {
-    const int n_outer = rd<true>(&e.p->n_outer_ops);
-    const ray r = ops_in<true>(e, rw, 0, n_outer);
-    double t1, t2;
+// Both boundary probes of a one-sphere boundary from one quadratic.
+// Measured (1 MI355X, A/B, profiles/r04/ab_pin_quad_boxrcp.log): C5 slice
+// 656.1 vs 639.3 Msamples/s.
 #ifndef RTW_MEDIUM_ONE_QUADRATIC
 #define RTW_MEDIUM_ONE_QUADRATIC 1
 #endif
+// The boundary distances of constant_medium::hit (hittable.h:438-449): the
+// closest boundary hit t1 in (-DBL_MAX, DBL_MAX), then the closest beyond
+// t1 + 0.0001f; false when either probe misses.  `r` is the ray in the
+// frame of the transforms enclosing the medium.
+template <int F, class STK>
+RTW_D bool medium_bounds(const scene& S, const entry_v& e, const ray& r, int n_outer, double& t1, double& t2,
+                         STK& stk) {
     if (RTW_MEDIUM_ONE_QUADRATIC && e.n_prims == 1 && e.bvh_root < 0 && is_sphere(ld(&S.prims[e.first_prim].type))) {
         // A boundary that is one sphere (wave-uniform: the media walk's
         // entries are): both probes (hittable.h:438-449) are that sphere's
@@ -1635,6 +1696,37 @@ RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_mi
         if (!boundary_t<F>(S, e, r, -kDblMax, kDblMax, t1, stk)) return false;
         if (!boundary_t<F>(S, e, r, t1 + kStep, kDblMax, t2, stk)) return false;
     }
+    return true;
+}
+
+// constant_medium::hit hittable.h:430-479 (at most one draw per call), in
+// the frame of the transforms enclosing the medium (translate / rotate_y
+// hand it their moved ray, hittable.h:299-311, 373-404)
+template <int F, class STK>
+RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_min, double t_max, uint32_t& rng,
+                    double& t_out, STK& stk, int visit = 0, volatile double* cache = nullptr) {
+    const int n_outer = rd<true>(&e.p->n_outer_ops);
+    const ray r = ops_in<true>(e, rw, 0, n_outer);
+    double t1, t2;
+#ifndef RTW_MEDIUM_CACHE
+#define RTW_MEDIUM_CACHE 1
+#endif
+    // boundary cache (scene::media visits): a later visit of this medium on
+    // the same ray reads the distances its first visit found (NaN: no
+    // boundary hit); the slot is wave-uniform, the cache a per-lane scratch
+    // array (stored once, read once: cheaper than the probes it replaces)
+    const int slot = RTW_MEDIUM_CACHE && cache ? ((visit >> kVisitSlotShift) & 15) - 1 : -1;
+    if (slot >= 0 && (visit & kVisitReuse)) {
+        t1 = cache[2 * slot];
+        t2 = cache[2 * slot + 1];
+        if (!(t1 == t1)) return false;
+    } else if (!medium_bounds<F>(S, e, r, n_outer, t1, t2, stk)) {
+        if (slot >= 0) cache[2 * slot] = __builtin_nan("");
+        return false;
+    } else if (slot >= 0) {
+        cache[2 * slot] = t1;
+        cache[2 * slot + 1] = t2;
+    }
     if (t1 < t_min) t1 = t_min;
     if (t2 > t_max) t2 = t_max;
     if (t1 >= t2) return false;
@@ -1648,6 +1740,7 @@ RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_mi
     }
     return false;
 }
+
 
 #ifdef RTW_PROF_WALK
 __device__ unsigned long long g_walk[32][64];  // clock per media-walk position (sampled walks), per lane slot
@@ -1817,12 +1910,14 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             const bool pw = (rng & 63) == 0;  // a sample of the walks
             uint64_t pw_t = pw ? clock64() : 0;
 #endif
+            volatile double cache[2 * kMediumSlots];  // medium boundary distances by slot (scratch)
             for (int k = 0; k < S.n_media; ++k) {
-                const int ei = ld(&S.media[k]);
+                const int visit = ld(&S.media[k]);
+                const int ei = visit & kVisitEntry;
                 const entry_v e = view_entry<true>(S, ei);
                 if (e.kind == RTW_ENTRY_MEDIUM) {
                     double t;
-                    if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk)) {
+                    if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk, visit, cache)) {
                         h.t = t;
                         h.prim = -(2 + ei);
                         h.rect = false;

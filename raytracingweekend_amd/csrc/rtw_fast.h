@@ -534,7 +534,7 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
         // the media walk: entries in the reference's visit order, media
         // drawn again in the second walk
         for (int k = 0; k < S.n_media; ++k) {
-            const int ei = ld(&S.media[k]);
+            const int ei = ld(&S.media[k]) & rtwd::kVisitEntry;  // (the fp64 walk's cache slots unused here)
             const ent_v e = view_entry<true>(S, ei);
             if (e.kind == RTW_ENTRY_MEDIUM) {
                 float t;

@@ -1977,6 +1977,26 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             for (int e = 0; e < d->n_entries; ++e)
                 if (d->entries[e].kind == RTW_ENTRY_MEDIUM) media.push_back(e);
         }
+        // boundary cache slots (rtw_device.h media_visit): a medium visited
+        // again later in the walk (the reference's second list walk) reuses
+        // the boundary distances its first visit found on the same ray; the
+        // first kMediumSlots media visited twice get a slot
+        std::map<int, int> slot_of, seen;
+        for (int32_t e : media)
+            if (d->entries[e].kind == RTW_ENTRY_MEDIUM) ++seen[e];
+        for (int32_t& v : media) {
+            const int e = v;
+            if (d->entries[e].kind != RTW_ENTRY_MEDIUM || seen[e] < 2) continue;
+            auto it = slot_of.find(e);
+            if (it == slot_of.end()) {
+                if ((int)slot_of.size() >= kMediumSlots) continue;
+                const int slot = (int)slot_of.size();
+                slot_of[e] = slot;
+                v = e | ((slot + 1) << kVisitSlotShift);  // first visit: fills the slot
+            } else {
+                v = e | ((it->second + 1) << kVisitSlotShift) | kVisitReuse;  // later visit: reads it
+            }
+        }
     }
     struct part {
         const void* src;
@@ -2803,8 +2823,11 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
             launch_pk<FF, MM, LL>(probe, name, cus, shm, st, S, J, C, base, bytes, stack_need); \
             return true;                                                                       \
         }
+        // Measured (1 MI355X, A/B, profiles/r04/ab_pin_quad_boxrcp.log): C5
+        // slice 656.1 vs 644.8 Msamples/s (the packet then holds all 1 668 of
+        // Book 2's nodes); C3 2 918 vs 2 933 (its 969 nodes fit already): the
+        // Book-2 kernel only.
 #ifndef RTW_SUBSET
-        RTW_PIN(F_WBVH | F_NOLIGHTS | F_PIN, SF_METAL | SF_DIEL, false)
         RTW_PIN(F_MEDIA | F_GBVH | F_LIGHTS | F_BLACK | F_PIN, SF_NOCHECKER, false)
 #endif
 #undef RTW_PIN
