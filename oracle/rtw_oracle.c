@@ -626,10 +626,14 @@ static v3 sample(const rtw_scene_desc* S, const rtw_camera_desc* cam, int nx, in
     return color(S, &r, max_depth, &g, tc);
 }
 
-int rtw_oracle_render(const rtw_scene_desc* S, const rtw_camera_desc* cam, int nx, int ny, int row_begin,
-                      int row_count, int spp_begin, int spp_count, int max_depth, uint64_t seed, int threads,
-                      double* sums, uint64_t* segments) {
-    if (!S || !cam || !sums || nx <= 0 || ny <= 0) return -1;
+/* Rows row_begin, row_begin + row_stride, ... (row_count of them), one
+ * OpenMP task per row: the bounded CPU sample bench.py times (every
+ * stride-th row of the image) in one multithreaded call. */
+int rtw_oracle_render_strided(const rtw_scene_desc* S, const rtw_camera_desc* cam, int nx, int ny, int row_begin,
+                              int row_stride, int row_count, int spp_begin, int spp_count, int max_depth,
+                              uint64_t seed, int threads, double* sums, uint64_t* segments) {
+    if (!S || !cam || !sums || nx <= 0 || ny <= 0 || row_stride <= 0 || row_count < 0) return -1;
+    if (row_count > 0 && (row_begin < 0 || row_begin + (int64_t)(row_count - 1) * row_stride >= ny)) return -1;
     if (S->has_perlin && (!S->perlin_ranvec || !S->perlin_perm)) return -1;
     uint64_t seg_total = 0;
 #ifdef _OPENMP
@@ -638,7 +642,8 @@ int rtw_oracle_render(const rtw_scene_desc* S, const rtw_camera_desc* cam, int n
     (void)threads;
 #endif
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : seg_total)
-    for (int j = row_begin; j < row_begin + row_count; j++) {
+    for (int k = 0; k < row_count; k++) {
+        const int j = row_begin + k * row_stride;
         trace_ctx tc = {0, 0, 0, 0};
         for (int i = 0; i < nx; i++) {
             v3 sum = mk(0, 0, 0);
@@ -651,6 +656,13 @@ int rtw_oracle_render(const rtw_scene_desc* S, const rtw_camera_desc* cam, int n
     }
     if (segments) *segments = seg_total;
     return 0;
+}
+
+int rtw_oracle_render(const rtw_scene_desc* S, const rtw_camera_desc* cam, int nx, int ny, int row_begin,
+                      int row_count, int spp_begin, int spp_count, int max_depth, uint64_t seed, int threads,
+                      double* sums, uint64_t* segments) {
+    return rtw_oracle_render_strided(S, cam, nx, ny, row_begin, 1, row_count, spp_begin, spp_count, max_depth,
+                                     seed, threads, sums, segments);
 }
 
 int rtw_oracle_trace(const rtw_scene_desc* S, const rtw_camera_desc* cam, int nx, int ny, int i, int j, int s,

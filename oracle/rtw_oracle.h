@@ -27,6 +27,12 @@ int rtw_oracle_render(const rtw_scene_desc* scene, const rtw_camera_desc* cam, i
                       int row_count, int spp_begin, int spp_count, int max_depth, uint64_t seed, int threads,
                       double* sums, uint64_t* segments);
 
+/* The same over rows row_begin + k*row_stride, k in [0, row_count): one
+ * multithreaded call over a strided sample of the image (bench.py). */
+int rtw_oracle_render_strided(const rtw_scene_desc* scene, const rtw_camera_desc* cam, int nx, int ny,
+                              int row_begin, int row_stride, int row_count, int spp_begin, int spp_count,
+                              int max_depth, uint64_t seed, int threads, double* sums, uint64_t* segments);
+
 /* One path, with its segments recorded (origin, direction, time, hit t,
  * hit flag) for debugging parity: at most max_seg rows of 8 doubles. */
 int rtw_oracle_trace(const rtw_scene_desc* scene, const rtw_camera_desc* cam, int nx, int ny, int i, int j, int s,

@@ -28,6 +28,10 @@ def oracle():
         L.rtw_oracle_render.argtypes = [C.POINTER(_abi.rtw_scene_desc), C.POINTER(_abi.rtw_camera_desc), C.c_int,
                                         C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int,
                                         C.c_void_p, C.POINTER(C.c_uint64)]
+        L.rtw_oracle_render_strided.restype = C.c_int
+        L.rtw_oracle_render_strided.argtypes = [C.POINTER(_abi.rtw_scene_desc), C.POINTER(_abi.rtw_camera_desc),
+                                                C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                C.c_int, C.c_uint64, C.c_int, C.c_void_p, C.POINTER(C.c_uint64)]
         L.rtw_oracle_trace.restype = C.c_int
         L.rtw_oracle_trace.argtypes = [C.POINTER(_abi.rtw_scene_desc), C.POINTER(_abi.rtw_camera_desc), C.c_int,
                                        C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
@@ -46,14 +50,16 @@ def oracle():
 
 def oracle_sums(scene_desc, nx, ny, spp, max_depth, seed=0, threads=0, rows=None, spp_begin=0, spp_count=None,
                 camera=None):
-    """Per-pixel radiance sums (nx*ny*3 float64) from the C restatement."""
+    """Per-pixel radiance sums (nx*ny*3 float64) from the C restatement.
+    rows: (begin, count) or (begin, count, stride) -- rows begin + k*stride."""
     out = np.zeros(nx * ny * 3, dtype=np.float64)
     seg = C.c_uint64(0)
-    r0, rc = (0, ny) if rows is None else rows
+    r0, rc, rs = (0, ny, 1) if rows is None else (tuple(rows) + (1,))[:3]
     cnt = spp if spp_count is None else spp_count
     cam = camera if camera is not None else scene_desc.camera
-    rcode = oracle().rtw_oracle_render(scene_desc.ptr, C.byref(cam), nx, ny, r0, rc, spp_begin, cnt, max_depth,
-                                       seed, threads, out.ctypes.data_as(C.c_void_p), C.byref(seg))
+    rcode = oracle().rtw_oracle_render_strided(scene_desc.ptr, C.byref(cam), nx, ny, r0, rs, rc, spp_begin, cnt,
+                                               max_depth, seed, threads, out.ctypes.data_as(C.c_void_p),
+                                               C.byref(seg))
     assert rcode == 0
     return out, seg.value
 

@@ -172,3 +172,34 @@ def test_cpu_baseline_sample_is_bounded(bench, monkeypatch):
         nx, ny = {"cornell_box": (800, 800), "random_balls": (1200, 800), "book2_final": (1600, 1600)}[scene]
         samples = nx * len(range(0, ny, stride)) * spp
         assert samples <= 25_000_000, scene
+
+
+def test_cpu_baseline_port_is_one_threaded_call(bench, monkeypatch, built):
+    """Without oracle/_ref/rtw_ref the C restatement is timed in ONE call over
+    the strided rows with every requested thread (it was one call
+    per row), and the strided call renders exactly the rows one-row calls do."""
+    import numpy as np
+    monkeypatch.syspath_prepend(str(ROOT / "tests"))
+    import oracle_lib
+    from raytracingweekend_amd.render import SceneDesc
+    calls = []
+    real = oracle_lib.oracle_sums
+
+    def spy(*a, **k):
+        calls.append(k)
+        return real(*a, **k)
+    monkeypatch.setattr(oracle_lib, "oracle_sums", spy)
+    a = parse(bench, monkeypatch, "--scene", "cornell_box", "--nx", "32", "--ny", "24", "--cpu-spp", "2")
+    out = bench.cpu_baseline(a, 4, use_reference=False)
+    assert out["kind"] == "port" and out["cores"] == 4 and out["value"] > 0
+    assert len(calls) == 1 and calls[0]["threads"] == 4 and calls[0]["rows"] == (0, 24, 1)
+
+    sd = SceneDesc("random_balls", 1.5, False)
+    strided, seg = real(sd, 24, 16, 2, 10, 3, threads=4, rows=(1, 4, 4))
+    rowwise = np.zeros_like(strided)
+    segs = 0
+    for j in (1, 5, 9, 13):
+        r, s = real(sd, 24, 16, 2, 10, 3, threads=1, rows=(j, 1))
+        rowwise += r
+        segs += s
+    assert seg == segs and np.array_equal(strided, rowwise)
