@@ -1117,8 +1117,11 @@ RTW_D void arbitrate_a(const scene& S, int pi, const ray& r, double t_min, hit_s
 // only when one of the wave's leaves holds such an item.  Quotients are
 // bit-identical under the rules of make_rect_rcp / walk_quot with t_min >=
 // 0.001; other lanes (and boundary probes) divide exactly.
+// Measured (profiles/r04/ab_cache_leafrcp.log): C5 slice -8 % with the
+// medium cache, -7 % without it (the kernel spills 29 VGPRs instead of 19):
+// off; -DRTW_LEAF_RCP=1 selects it.
 #ifndef RTW_LEAF_RCP
-#define RTW_LEAF_RCP 1
+#define RTW_LEAF_RCP 0
 #endif
 RTW_D void leaf_items(const scene& S, int la, int lc, const ray& r, double t_min, hit_state& h, double fc) {
     if constexpr (!RTW_LEAF_RCP || RTW_BOX_NEAR) {
@@ -1708,8 +1711,8 @@ RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_mi
     const int n_outer = rd<true>(&e.p->n_outer_ops);
     const ray r = ops_in<true>(e, rw, 0, n_outer);
     double t1, t2;
-#ifndef RTW_MEDIUM_CACHE
-#define RTW_MEDIUM_CACHE 1
+#ifndef RTW_MEDIUM_CACHE  // measured -8 % on the C5 slice (ab_cache_leafrcp.log: its scratch array): off
+#define RTW_MEDIUM_CACHE 0
 #endif
     // boundary cache (scene::media visits): a later visit of this medium on
     // the same ray reads the distances its first visit found (NaN: no
@@ -1910,7 +1913,11 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             const bool pw = (rng & 63) == 0;  // a sample of the walks
             uint64_t pw_t = pw ? clock64() : 0;
 #endif
+#if RTW_MEDIUM_CACHE
             volatile double cache[2 * kMediumSlots];  // medium boundary distances by slot (scratch)
+#else
+            volatile double* const cache = nullptr;
+#endif
             for (int k = 0; k < S.n_media; ++k) {
                 const int visit = ld(&S.media[k]);
                 const int ei = visit & kVisitEntry;
