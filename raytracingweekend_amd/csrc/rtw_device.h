@@ -202,6 +202,18 @@ RTW_HD d3 local(const onb& b, d3 a) { return b.u * a.x + b.v * a.y + b.w * a.z; 
 // WORLD_RUN_YSPHERES: the same, all spheres for ysphere_scan.
 enum : int { WORLD_RUN_PLAIN = -1, WORLD_RUN_YSPHERES = -2 };
 struct bvh_node32;
+struct bvh_node16;
+// Device BVH node format (rtw_scene_upload writes it, node_at reads it):
+// 32-B nodes with fp32 bounds, or (RTW_NODE16) 16-B nodes with fp16 bounds
+// scaled by a power of two, so the LDS node packet holds twice the nodes.
+#ifndef RTW_NODE16
+#define RTW_NODE16 0
+#endif
+#if RTW_NODE16
+using node_store = bvh_node16;
+#else
+using node_store = bvh_node32;
+#endif
 struct world_run {
     int32_t entry, first_prim, n_prims, movers;  // movers: the prims hold DP_MOVING_COMMON*
 };
@@ -237,7 +249,7 @@ struct scene {
     const rtw_material* materials;
     const rtw_texture* textures;
     const rtw_light* lights;
-    const bvh_node32* nodes;  // device BVH nodes (fp32 bounds, rtw_scene_upload)
+    const node_store* nodes;  // device BVH nodes (rtw_scene_upload)
     const int32_t* items;
     const double* ranvec;
     const int32_t* perm;
@@ -255,6 +267,7 @@ struct scene {
     double mv_t0, mv_den;  // their time0 and time1 - time0
     int32_t fast_div;      // shared-divisor sphere roots allowed in world walks (ysphere_scan)
     double bvh_bound;      // largest |coordinate| of any device BVH node (make_slab_ray)
+    double node_scale;     // RTW_NODE16: a node's fp16 bounds are its coordinates / node_scale (a power of 2)
     // ysphere_scan's fp32 prefilter: per prim {cx, cy, cz, dy, r^2, 0, 0, 0}
     // (r^2 = +inf: never filtered), and the largest |cx|, |cy|, |dy|, |cz|
     // and r^2 of the filtered spheres
@@ -264,7 +277,7 @@ struct scene {
     // BVH breadth-first from all roots together, so nodes [0, n_lnodes) are
     // the top levels of every tree; the persistent BVH kernels copy them to
     // LDS (lnodes) once per workgroup (n_lnodes = 0: all from memory)
-    const bvh_node32* lnodes;
+    const node_store* lnodes;
     int32_t n_lnodes;
     int32_t n_nodes;  // device BVH nodes in all
     // The same BVHs with 4-wide nodes (bvh_node4, rtw_scene_upload collapses
@@ -1162,6 +1175,28 @@ struct bvh_node32 {
     int32_t b;  // inner: right child | pad << 28 (push_children); leaf: -count
 };
 RTW_HD int node_count(const bvh_node32& n) { return n.b < 0 ? -n.b : 0; }
+// The 16-B form (RTW_NODE16): bounds as fp16 of coordinate * 2^k (rounded
+// outward at upload; scene::node_scale = 2^-k), w = index (24 bits) | meta
+// << 24: a leaf's first item and meta 0x80 | count (count < 128); an inner
+// node's left child -- the right one is the next node (breadth-first
+// numbering puts siblings together) -- and meta = its split bits (pad).
+struct bvh_node16 {
+    uint16_t lo[3], hi[3];
+    uint32_t w;
+};
+constexpr uint32_t kNode16Leaf = 0x80u;
+// the 16-B node as the walks read it: fp32 bounds in the scaled space (the
+// slab ray's reciprocals carry node_scale), children / items as bvh_node32's
+RTW_D float half_bits(uint32_t h) { return (float)__builtin_bit_cast(_Float16, (uint16_t)h); }
+RTW_D bvh_node32 decode16(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+    bvh_node32 nd;
+    nd.lo[0] = half_bits(x & 0xffff), nd.lo[1] = half_bits(x >> 16), nd.lo[2] = half_bits(y & 0xffff);
+    nd.hi[0] = half_bits(y >> 16), nd.hi[1] = half_bits(z & 0xffff), nd.hi[2] = half_bits(z >> 16);
+    const int idx = (int)(w & 0xffffffu), meta = (int)(w >> 24);
+    nd.a = idx;
+    nd.b = (meta & kNode16Leaf) ? -(meta & 0x7f) : ((idx + 1) | (meta << 28));
+    return nd;
+}
 
 // Per-walk fp32 form of the ray for the slab tests: t = x * inv + oi per
 // axis, with oi = -o * inv moved down (oin, near planes) and up (oif, far
@@ -1185,8 +1220,17 @@ RTW_D slab_ray make_slab_ray(const scene& S, const ray& r) {
         const double inv = 1.0 / dd[k];
         const double oi = -oo[k] * inv;
         const double eps = 0x1.8p-21 * (S.bvh_bound + __builtin_fabs(oo[k])) * __builtin_fabs(inv) + 0x1p-120;
+#if RTW_NODE16
+        // node coordinates x = h * node_scale: x * inv = h * (inv * node_scale)
+        // exactly while inv * node_scale stays a normal float (power-of-2 scale)
+        const double invs = inv * S.node_scale;
+        const bool ok = __builtin_fabs(inv) <= 0x1p90 && eps <= 0x1p90 && __builtin_fabs(invs) <= 0x1p100 &&
+                        __builtin_fabs(invs) >= 0x1p-100;
+        s.inv[k] = ok ? (float)invs : 0.0f;
+#else
         const bool ok = __builtin_fabs(inv) <= 0x1p90 && eps <= 0x1p90;
         s.inv[k] = ok ? (float)inv : 0.0f;
+#endif
         s.oin[k] = ok ? (float)(oi - eps) : -__builtin_inff();
         s.oif[k] = ok ? (float)(oi + eps) : __builtin_inff();
     }
@@ -1272,6 +1316,14 @@ RTW_D bvh_node32 node_at(const scene& S, int i) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     using lds_v4 = const __attribute__((address_space(3))) v4u;
     using glb_v4 = const __attribute__((address_space(1))) v4u;
+#if RTW_NODE16
+    v4u a;
+    if (i < S.n_lnodes)
+        a = *(lds_v4*)(S.lnodes + i);
+    else
+        a = *(glb_v4*)(S.nodes + i);
+    return decode16(a.x, a.y, a.z, a.w);
+#else
     v4u a, b;
     if (i < S.n_lnodes) {
         lds_v4* p = (lds_v4*)(S.lnodes + i);
@@ -1285,6 +1337,7 @@ RTW_D bvh_node32 node_at(const scene& S, int i) {
     __builtin_memcpy(&nd, &a, 16);
     __builtin_memcpy(reinterpret_cast<char*>(&nd) + 16, &b, 16);
     return nd;
+#endif
 }
 
 // 4-wide BVH node (rtw_scene_upload collapses each binary tree: a node's
@@ -1326,6 +1379,10 @@ RTW_D bvh_node4 node4_at(const scene& S, int i) {
 // A node at a wave-uniform index (packet walks): scalar loads through the
 // scalar cache, the fields land in SGPRs.
 RTW_D bvh_node32 node_s(const scene& S, int i) {
+#if RTW_NODE16
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(S.nodes + i);
+    return decode16(ld(p), ld(p + 1), ld(p + 2), ld(p + 3));
+#else
     bvh_node32 nd;
     const bvh_node32* p = S.nodes + i;
 #pragma unroll
@@ -1333,6 +1390,7 @@ RTW_D bvh_node32 node_s(const scene& S, int i) {
     nd.a = ld(&p->a);
     nd.b = ld(&p->b);
     return nd;
+#endif
 }
 
 // Inner nodes carry their children's split axis (pad & 3) and whether the
@@ -1389,7 +1447,23 @@ template <class STK>
 RTW_D bool expand_children(const scene& S, const slab_ray& sr, float t0, float t1, int dneg, STK& stk, int& sp,
                            int& ca, int& cb) {
     const int pad = cb >> 28, right = cb & 0x0fffffff;
+#if RTW_NODE16
+    // siblings are adjacent 16-B nodes: one 32-B read for both
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    using lds_v4 = const __attribute__((address_space(3))) v4u;
+    using glb_v4 = const __attribute__((address_space(1))) v4u;
+    v4u qa, qb;
+    if (right < S.n_lnodes) {
+        lds_v4* p = (lds_v4*)(S.lnodes + ca);
+        qa = p[0], qb = p[1];
+    } else {
+        glb_v4* p = (glb_v4*)(S.nodes + ca);
+        qa = p[0], qb = p[1];
+    }
+    const bvh_node32 L = decode16(qa.x, qa.y, qa.z, qa.w), R = decode16(qb.x, qb.y, qb.z, qb.w);
+#else
     const bvh_node32 L = node_at(S, ca), R = node_at(S, right);
+#endif
     const bool hl = slab32(L, sr, t0, t1), hr = slab32(R, sr, t0, t1);
     const bool left_first = (((dneg >> (pad & 3)) ^ (pad >> 2)) & 1) == 0;
     const bool hn = left_first ? hl : hr, hf = left_first ? hr : hl;

@@ -104,7 +104,7 @@ struct fscene {
     const float* ranvec;    // 256 x 3
     const int32_t* perm;    // 3 x 256
     const float* frames;    // per rect prim: world-normal onb (u, v, w)
-    const bvh_node32* nodes;
+    const rtwd::node_store* nodes;
     const int32_t* items;
     const world_run* runs;
     const int32_t* media;
@@ -114,8 +114,9 @@ struct fscene {
     int32_t n_lights, world_bvh_root, render_type, background, n_media, n_runs, n_nodes;
     // the BVH node packet in LDS (k_fast with LDS stacks: the top n_lnodes
     // nodes of the BFS numbering, set by the kernel; 0 elsewhere)
-    const bvh_node32* lnodes;
+    const rtwd::node_store* lnodes;
     int32_t n_lnodes;
+    float node_scale;  // RTW_NODE16: rtwd::scene::node_scale
 };
 
 // uniform (scalar) loads of a prim's fields
@@ -340,10 +341,15 @@ RTW_D void arbitrate_item(const fscene& S, int it, const fray& r, float tmin, fh
 struct slab_rayf {
     f3 inv, oi;  // t = x * inv + oi per axis
 };
-RTW_D slab_rayf make_slab(const fray& r) {
+RTW_D slab_rayf make_slab(const fscene& S, const fray& r) {
     slab_rayf s;
     s.inv = f3{rcp(r.d.x), rcp(r.d.y), rcp(r.d.z)};
     s.oi = f3{-r.o.x * s.inv.x, -r.o.y * s.inv.y, -r.o.z * s.inv.z};
+#if RTW_NODE16
+    s.inv = s.inv * S.node_scale;  // the nodes' fp16 bounds are coordinates / node_scale
+#else
+    (void)S;
+#endif
     return s;
 }
 RTW_D bool slab(const bvh_node32& nd, const slab_rayf& s, float t0, float t1) {
@@ -362,6 +368,14 @@ RTW_D bvh_node32 node_at(const fscene& S, int i) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     using lds_v4 = const __attribute__((address_space(3))) v4u;
     using glb_v4 = const __attribute__((address_space(1))) v4u;
+#if RTW_NODE16
+    v4u a;
+    if (i < S.n_lnodes)
+        a = *(lds_v4*)(S.lnodes + i);
+    else
+        a = *(glb_v4*)(S.nodes + i);
+    return rtwd::decode16(a.x, a.y, a.z, a.w);
+#else
     v4u a, b;
     if (i < S.n_lnodes) {
         lds_v4* p = (lds_v4*)(S.lnodes + i);
@@ -375,6 +389,7 @@ RTW_D bvh_node32 node_at(const fscene& S, int i) {
     __builtin_memcpy(&nd, &a, 16);
     __builtin_memcpy(reinterpret_cast<char*>(&nd) + 16, &b, 16);
     return nd;
+#endif
 }
 
 // Speculative while-while for the fp32 world walk (RTW_SPEC_WALK's form
@@ -408,7 +423,7 @@ struct priv_stackf {
 
 template <class STK>
 RTW_D void group_bvh(const fscene& S, int root, const fray& r, float tmin, fhit& h, STK& stk, int base) {
-    const slab_rayf sr = make_slab(r);
+    const slab_rayf sr = make_slab(S, r);
     const float t0 = tmin > 0 ? tmin * 0.5f : tmin * 2.0f - 1e-6f;
     int sp = base;
     stk.at(sp++) = root;
@@ -465,7 +480,7 @@ template <int F, class STK>
 RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk) {
     fhit h{kFltMaxF, -1, false};
     if constexpr ((F & rtwd::F_WBVH) != 0 && (F & rtwd::F_MEDIA) == 0) {
-        const slab_rayf sr = make_slab(r);
+        const slab_rayf sr = make_slab(S, r);
         const float t0 = kTMinF * 0.5f;
         int sp = 0;
         stk.at(sp++) = S.world_bvh_root;

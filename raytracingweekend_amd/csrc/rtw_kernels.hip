@@ -783,7 +783,7 @@ void k_persist(persist_args) {
         const persist_args& A = args_now();
         const uint4* src = reinterpret_cast<const uint4*>(RTW_BVH4 ? (const void*)A.S.nodes4 : (const void*)A.S.nodes);
         uint4* dst = reinterpret_cast<uint4*>(s_scene + A.lds_nodes_off);
-        constexpr uint32_t kNode16 = (uint32_t)((RTW_BVH4 ? sizeof(bvh_node4) : sizeof(bvh_node32)) / 16);
+        constexpr uint32_t kNode16 = (uint32_t)((RTW_BVH4 ? sizeof(bvh_node4) : sizeof(node_store)) / 16);
         for (uint32_t k = threadIdx.x; k < A.lds_nodes * kNode16; k += kPBlock) dst[k] = src[k];
     }
     if (LDS || LST) __syncthreads();
@@ -959,7 +959,7 @@ void k_persist(persist_args) {
                     S.lnodes4 = reinterpret_cast<const bvh_node4*>(s_scene + A.lds_nodes_off);
                     S.n_lnodes4 = (int32_t)A.lds_nodes;
                 } else {
-                    S.lnodes = reinterpret_cast<const bvh_node32*>(s_scene + A.lds_nodes_off);
+                    S.lnodes = reinterpret_cast<const node_store*>(s_scene + A.lds_nodes_off);
                     S.n_lnodes = (int32_t)A.lds_nodes;
                 }
                 lds_stack stk{&s_stack[0][tid]};
@@ -1352,7 +1352,8 @@ void k_fast(fast_args) {
         const fast_args& A = fast_args_now();
         const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
         uint4* dst = reinterpret_cast<uint4*>(s_nodes);
-        for (uint32_t k = threadIdx.x; k < A.lds_nodes * 2; k += kFastBlock) dst[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < A.lds_nodes * (uint32_t)(sizeof(node_store) / 16); k += kFastBlock)
+            dst[k] = src[k];
         __syncthreads();
     }
     const uint32_t lane = threadIdx.x & 63;
@@ -1410,7 +1411,7 @@ void k_fast(fast_args) {
             lds_stackf stk{&s_stack[0][threadIdx.x]};
             const fast_args& A = fast_args_now();
             fscene S = A.S;
-            S.lnodes = reinterpret_cast<const bvh_node32*>(s_nodes);
+            S.lnodes = reinterpret_cast<const node_store*>(s_nodes);
             S.n_lnodes = (int32_t)A.lds_nodes;
             h = world_closest<F>(S, r, rng, stk);
         } else {
@@ -2348,6 +2349,63 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         // 16-bit LDS stack entries: node4 ids >= 0, ~leaf < 0
         bvh4_ok = bvh4_ok && n4.size() < 32768 && leaf4.size() < 32768;
     }
+    // 16-B nodes (RTW_NODE16, rtw_device.h bvh_node16): the fp32 bounds times
+    // 2^k, k the largest with bvh_bound * 2^k <= 2^15, rounded outward to
+    // fp16 (exact products: a power-of-2 scale); bvh_bound becomes the
+    // largest |coordinate| the fp16 bounds stand for.  A tree the format
+    // cannot hold (siblings apart -- a node shared by two parents --, leaves
+    // of 128+ items, 2^24+ nodes or items) is not used (the flat list gives
+    // the same image).
+    std::vector<bvh_node16> dnodes16;
+    double node_scale = 1.0;
+    if (RTW_NODE16 && bvh_ok && !dnodes32.empty()) {
+        int k = 0;
+        if (bvh_bound > 0) std::frexp(0x1p15 / bvh_bound, &k), k -= 1;  // 2^k <= 2^15 / bound
+        k = std::max(-100, std::min(100, k));
+        const double up = std::ldexp(1.0, k);
+        node_scale = std::ldexp(1.0, -k);
+        auto half_out = [](double v, bool up_dir) -> uint16_t {  // fp16 bits of v rounded toward -inf / +inf
+            _Float16 h = (_Float16)v;
+            uint16_t b = __builtin_bit_cast(uint16_t, h);
+            const double hv = (double)h;
+            if (up_dir ? hv < v : hv > v) {
+                const bool neg = (b & 0x8000) != 0;
+                if ((b & 0x7fff) == 0) b = up_dir ? 0x0001 : 0x8001;  // +-0 -> the smallest subnormal outward
+                else if (neg == up_dir) b = (uint16_t)(b - 1);       // toward zero
+                else b = (uint16_t)(b + 1);                          // away from zero
+            }
+            return b;
+        };
+        bool ok16 = dnodes32.size() < (1u << 24) && ditems.size() < (1u << 24);
+        double bound16 = 0.0;
+        dnodes16.resize(dnodes32.size());
+        for (size_t n = 0; n < dnodes32.size() && ok16; ++n) {
+            const bvh_node32& M = dnodes32[n];
+            bvh_node16& Q = dnodes16[n];
+            for (int j = 0; j < 3; ++j) {
+                Q.lo[j] = half_out((double)M.lo[j] * up, false);
+                Q.hi[j] = half_out((double)M.hi[j] * up, true);
+                for (uint16_t b : {Q.lo[j], Q.hi[j]}) {
+                    const double x = (double)__builtin_bit_cast(_Float16, b);
+                    ok16 = ok16 && std::isfinite(x);
+                    bound16 = std::max(bound16, std::fabs(x) * node_scale);
+                }
+            }
+            if (M.b < 0) {
+                ok16 = ok16 && -M.b < 128 && M.a >= 0;
+                Q.w = (uint32_t)M.a | ((kNode16Leaf | (uint32_t)(-M.b)) << 24);
+            } else {
+                ok16 = ok16 && (M.b & 0x0fffffff) == M.a + 1;
+                Q.w = (uint32_t)M.a | ((uint32_t)(M.b >> 28) << 24);
+            }
+        }
+        if (ok16) {
+            bvh_bound = bound16;
+        } else {
+            bvh_ok = false;
+            dnodes16.clear();
+        }
+    }
     // device entries (dev_entry) and their op pool
     std::vector<dev_entry> dev_entries(std::max<size_t>(dentries.size(), 1));
     std::vector<dev_op> dev_ops;
@@ -2384,7 +2442,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {frames.data(), sizeof(double) * frames.size(), 0},
         {mat_aux.data(), sizeof(double) * mat_aux.size(), 0},
         {dev_ops.data(), sizeof(dev_op) * dev_ops.size(), 0},
-        {dnodes32.data(), sizeof(bvh_node32) * dnodes32.size(), 0},
+        {RTW_NODE16 ? (const void*)dnodes16.data() : (const void*)dnodes32.data(),
+         RTW_NODE16 ? sizeof(bvh_node16) * dnodes16.size() : sizeof(bvh_node32) * dnodes32.size(), 0},
         {ditems.data(), sizeof(int32_t) * ditems.size(), 0},
         {runs.data(), sizeof(world_run) * runs.size(), 0},
         {ysph.data(), sizeof(float) * ysph.size(), 0},
@@ -2416,8 +2475,9 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.prim_onb = (const double*)at(8);
     S.mat_aux = (const double*)at(9);
     S.ops = (const dev_op*)at(10);
-    S.nodes = (const bvh_node32*)at(11);
+    S.nodes = (const node_store*)at(11);
     S.bvh_bound = bvh_bound;
+    S.node_scale = node_scale;
     S.items = (const int32_t*)at(12);
     S.runs = (const world_run*)at(13);
     S.ysph = (const float*)at(14);
@@ -2450,7 +2510,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.n_lights = d->n_lights;
     S.light_weight = d->n_lights > 0 ? 1.0 / (double)d->n_lights : 0.0;
     S.world_bvh_root = bvh_ok ? world_root : -1;
-    S.n_nodes = (int32_t)dnodes32.size();
+    S.n_nodes = bvh_ok ? (int32_t)dnodes32.size() : 0;
     S.render_type = d->render_type;
     S.background = d->background;
     S.n_media = (int32_t)media.size();
@@ -2613,6 +2673,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         F.perm = p2[8].bytes ? (const int32_t*)(b2 + p2[8].off) : nullptr;
         h->f32_bytes = (uint32_t)(p2[8].off + p2[8].bytes);
         F.nodes = S.nodes;
+        F.node_scale = (float)S.node_scale;
         F.items = S.items;
         F.runs = S.runs;
         F.media = S.media;
@@ -2749,7 +2810,7 @@ bool sort_forced(bool& value) {
 // rtw_scene_query.
 thread_local uint32_t g_node_packet = 0;
 // the packet holds 4-wide nodes when the walks are 4-wide (RTW_BVH4)
-constexpr size_t kPacketNodeBytes = RTW_BVH4 ? sizeof(bvh_node4) : sizeof(bvh_node32);
+constexpr size_t kPacketNodeBytes = RTW_BVH4 ? sizeof(bvh_node4) : sizeof(node_store);
 template <int FF, int MM, bool LL>
 uint32_t node_packet(size_t shm, int n_nodes) {
     const char* e = std::getenv("RTW_LDS_NODES");
@@ -2894,7 +2955,7 @@ uint32_t fast_node_packet(const void* fn, int n_nodes) {
     uint32_t best = 0;
     for (uint32_t k = 32; k <= cap + 31; k += 32) {
         const uint32_t kk = std::min(k, cap);
-        if (blocks_per_cu(fn, rtwf::kFastBlock, kk * sizeof(bvh_node32)) < base) break;
+        if (blocks_per_cu(fn, rtwf::kFastBlock, kk * sizeof(node_store)) < base) break;
         best = kk;
         if (kk == cap) break;
     }
@@ -2911,7 +2972,7 @@ void launch_fast_t(bool probe, std::string* name, int cus, hipStream_t st, const
     const void* fn = reinterpret_cast<const void*>(&k_fast<FF, LST>);
     fast_args a = A;
     a.lds_nodes = LST ? fast_node_packet(fn, A.S.n_nodes) : 0u;
-    const size_t shm = (size_t)a.lds_nodes * sizeof(bvh_node32);
+    const size_t shm = (size_t)a.lds_nodes * sizeof(node_store);
     const int grid = grid_blocks(fn, rtwf::kFastBlock, shm, cus);
     hipLaunchKernelGGL((k_fast<FF, LST>), dim3(grid), dim3(rtwf::kFastBlock), shm, st, a);
 }
