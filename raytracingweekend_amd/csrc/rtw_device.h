@@ -1192,6 +1192,9 @@ RTW_D bvh_node32 decode16(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
     bvh_node32 nd;
     nd.lo[0] = half_bits(x & 0xffff), nd.lo[1] = half_bits(x >> 16), nd.lo[2] = half_bits(y & 0xffff);
     nd.hi[0] = half_bits(y >> 16), nd.hi[1] = half_bits(z & 0xffff), nd.hi[2] = half_bits(z >> 16);
+#if RTW_NODE16_CVT  // experiment: converted bounds (v_cvt_f32_f16) instead of v_fma_mix_f32 in the slab test
+    asm volatile("" : "+v"(nd.lo[0]), "+v"(nd.lo[1]), "+v"(nd.lo[2]), "+v"(nd.hi[0]), "+v"(nd.hi[1]), "+v"(nd.hi[2]));
+#endif
     const int idx = (int)(w & 0xffffffu), meta = (int)(w >> 24);
     nd.a = idx;
     nd.b = (meta & kNode16Leaf) ? -(meta & 0x7f) : ((idx + 1) | (meta << 28));

@@ -94,6 +94,10 @@ __global__ __launch_bounds__(256) void k_rate(double* out, unsigned seed) {
         if (K == 31) { BODY8(DSQRT) }
         if (K == 32) { BODY8(PKMUL) }
         if (K == 33) { BODY8(BFE) }
+#define FMIX(i) asm volatile("v_fma_mix_f32 %0, %0, %0, %0 op_sel_hi:[1,0,0]" : "+v"(f[i]));
+#define CVTH(i) asm volatile("v_cvt_f32_f16 %0, %0" : "+v"(f[i]));
+        if (K == 34) { BODY8(FMIX) }
+        if (K == 35) { BODY8(CVTH) }
     }
     double s = 0;
     for (int i = 0; i < 8; ++i) s += d[i] + (double)u[i] + (double)w[i] + (double)f[i];
@@ -106,7 +110,8 @@ static const char* kNames[] = {"v_fma_f64", "v_mul_f64", "v_add_f64", "v_rcp_f64
                                "v_cndmask_b32", "v_add_f32", "v_fma_f32", "v_pk_fma_f32",
                                "v_min3_f32", "v_min_f64", "v_cvt_f32_f64", "v_rcp_f32", "v_sqrt_f32",
                                "v_exp_f32", "v_sin_f32", "v_mov_b32", "v_cmp_lt_f32", "v_cndmask_b32 (sgpr)",
-                               "v_and_b32", "v_lshlrev_b32", "v_sqrt_f64", "v_pk_mul_f32", "v_bfe_u32"};
+                               "v_and_b32", "v_lshlrev_b32", "v_sqrt_f64", "v_pk_mul_f32", "v_bfe_u32",
+                               "v_fma_mix_f32", "v_cvt_f32_f16"};
 
 template <int K>
 static int run(double* out, int cus, double clk_ghz) {
@@ -152,6 +157,7 @@ int main() {
     run<28>(out, p.multiProcessorCount, clk); run<29>(out, p.multiProcessorCount, clk);
     run<30>(out, p.multiProcessorCount, clk); run<31>(out, p.multiProcessorCount, clk);
     run<32>(out, p.multiProcessorCount, clk); run<33>(out, p.multiProcessorCount, clk);
+    run<34>(out, p.multiProcessorCount, clk); run<35>(out, p.multiProcessorCount, clk);
     CHK(hipFree(out));
     return 0;
 }
