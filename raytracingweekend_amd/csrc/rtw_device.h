@@ -206,6 +206,14 @@ struct bvh_node16;
 // Device BVH node format (rtw_scene_upload writes it, node_at reads it):
 // 32-B nodes with fp32 bounds, or (RTW_NODE16) 16-B nodes with fp16 bounds
 // scaled by a power of two, so the LDS node packet holds twice the nodes.
+// Measured (1 MI355X, A/B, profiles/r04/ab_node16_r4e.log, ab_node16_r4f.log;
+// GPU suite green with it): C5 slice 613 vs 655, C3 2 684 vs 2 961, C3 fp32
+// 4 631 vs 5 156 Msamples/s.  The packet already holds all of C5's 1 668 and
+// C3's 969 nodes at 32 B (F_PIN), so only the decode is left: the slab test's
+// fp16 operands cost v_fma_mix_f32 at 4.4 cycles per wave instruction, or
+// v_cvt_f32_f16 at 4.3 + v_fma_f32 at 2.75 (converted bounds measured worse:
+// C3 2 582), against 2.75 for v_fma_f32 (profiles/r04/valu_rates_r4f.log).
+// Off; -DRTW_NODE16=1 selects it.
 #ifndef RTW_NODE16
 #define RTW_NODE16 0
 #endif
@@ -1192,9 +1200,6 @@ RTW_D bvh_node32 decode16(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
     bvh_node32 nd;
     nd.lo[0] = half_bits(x & 0xffff), nd.lo[1] = half_bits(x >> 16), nd.lo[2] = half_bits(y & 0xffff);
     nd.hi[0] = half_bits(y >> 16), nd.hi[1] = half_bits(z & 0xffff), nd.hi[2] = half_bits(z >> 16);
-#if RTW_NODE16_CVT  // experiment: converted bounds (v_cvt_f32_f16) instead of v_fma_mix_f32 in the slab test
-    asm volatile("" : "+v"(nd.lo[0]), "+v"(nd.lo[1]), "+v"(nd.lo[2]), "+v"(nd.hi[0]), "+v"(nd.hi[1]), "+v"(nd.hi[2]));
-#endif
     const int idx = (int)(w & 0xffffffu), meta = (int)(w >> 24);
     nd.a = idx;
     nd.b = (meta & kNode16Leaf) ? -(meta & 0x7f) : ((idx + 1) | (meta << 28));
