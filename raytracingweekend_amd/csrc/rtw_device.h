@@ -1217,6 +1217,15 @@ RTW_D bvh_node32 decode16(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
 // off by less than 2^-23.9 of that), and 2^-120 a flushed denormal result.
 // An axis whose |inv| or eps exceeds 2^90 (d.K ~ 0, NaN) never culls:
 // inv = 0, oin = -inf, oif = +inf.
+// RTW_SLAB_RCP32: inv is the hardware fp32 reciprocal of fl32(d) instead of
+// fl32(1.0 / d) -- within 2^-22.4 |1 / d| (2^-24 for the conversion, 1 ulp
+// for v_rcp_f32), and oi = -o * inv in fp64 within 2^-22.4 |o / d|; with the
+// final rounding of oi +- eps that is under 2^-21.9 (B + |o|) |1 / d|, inside
+// the 2^-21 part (eps itself computed from |inv| loses a 2^-22 relative) --
+// three fp64 divisions fewer per walk.
+#ifndef RTW_SLAB_RCP32
+#define RTW_SLAB_RCP32 1
+#endif
 struct slab_ray {
     float inv[3], oin[3], oif[3];
 };
@@ -1225,7 +1234,11 @@ RTW_D slab_ray make_slab_ray(const scene& S, const ray& r) {
     const double dd[3] = {r.d.x, r.d.y, r.d.z}, oo[3] = {r.o.x, r.o.y, r.o.z};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
+#if RTW_SLAB_RCP32
+        const double inv = (double)__builtin_amdgcn_rcpf((float)dd[k]);
+#else
         const double inv = 1.0 / dd[k];
+#endif
         const double oi = -oo[k] * inv;
         const double eps = 0x1.8p-21 * (S.bvh_bound + __builtin_fabs(oo[k])) * __builtin_fabs(inv) + 0x1p-120;
 #if RTW_NODE16
