@@ -250,6 +250,11 @@ constexpr int kMediumSlots = 4;
 constexpr int32_t kVisitSlotShift = 20;
 constexpr int32_t kVisitEntry = (1 << kVisitSlotShift) - 1;
 constexpr int32_t kVisitReuse = 1 << 24;
+// Fused group walks (fused_group_bvh): the visit of a group BVH marked
+// kVisitFuse walks scene::fuse_entry's BVH too, in the same loop; that
+// entry's own visit (kVisitMerge) then merges the result found for it.
+constexpr int32_t kVisitFuse = 1 << 25;
+constexpr int32_t kVisitMerge = 1 << 26;
 struct scene {
     const rtw_prim* prims;
     const dev_entry* entries;
@@ -276,6 +281,7 @@ struct scene {
     int32_t fast_div;      // shared-divisor sphere roots allowed in world walks (ysphere_scan)
     double bvh_bound;      // largest |coordinate| of any device BVH node (make_slab_ray)
     double node_scale;     // RTW_NODE16: a node's fp16 bounds are its coordinates / node_scale (a power of 2)
+    int32_t fuse_entry;    // the group BVH walked with the kVisitFuse visit's (-1: none)
     // ysphere_scan's fp32 prefilter: per prim {cx, cy, cz, dy, r^2, 0, 0, 0}
     // (r^2 = +inf: never filtered), and the largest |cx|, |cy|, |dy|, |cz|
     // and r^2 of the filtered spheres
@@ -1726,6 +1732,62 @@ RTW_D void group_bvh(const scene& S, int root, int root4, const ray& r, double t
 #endif
 }
 
+// Two group BVHs of the media walk in one while-while loop.  Walked one
+// after the other, a wave pays the longest ground walk of its lanes and then
+// the longest cluster walk; here a lane whose first walk ends moves on to the
+// second while the others continue, so the wave pays roughly the longest
+// SUM (scripts/sim_walk.py: Book 2's group steps per wave-segment 51 -> 35).
+// e0 has no ops (the world frame) and is visited first; e1, visited later
+// in the list, is walked now from the closest hit of e0 on: with the larger
+// t_max it finds the closest of its items beyond which nothing it holds can
+// win later, so its result (hb), merged at its own visit by better() --
+// the rule every item test applies, order-independent -- is the list order's
+// (a deterministic group: no draws; its nodes are culled only against a t
+// that bounds what could still win).
+#ifndef RTW_FUSE_GROUPS
+#define RTW_FUSE_GROUPS 1
+#endif
+template <class STK>
+RTW_D void fused_group_bvh(const scene& S, const entry_v& e0, const entry_v& e1, const ray& r, double t_min,
+                           hit_state& h, hit_state& hb, STK& stk) {
+    const float t0 = t_lo32(t_min);
+    slab_ray sr = make_slab_ray(S, r);
+    int dneg = dir_mask(r.d);
+    double fc = motion_frac(S, r.t, e0.movers);
+    int sp = 0;
+    stk.at(sp++) = e0.bvh_root;
+    bool second = false;
+    hit_state hg = h;
+    for (;;) {
+        int la = 0, lc = 0;
+        while (lc == 0) {
+            if (sp == 0) {
+                if (second) break;
+                second = true;  // e0 done: its winner bounds e1's walk
+                hg = h;
+                const ray r1 = entry_local_ray<true>(e1, r);
+                sr = make_slab_ray(S, r1);
+                dneg = dir_mask(r1.d);
+                fc = motion_frac(S, r.t, e1.movers);
+                stk.at(sp++) = e1.bvh_root;
+            }
+            const bvh_node32 nd = node_at(S, stk.at(--sp));
+            if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
+            lc = node_count(nd);
+            la = nd.a;
+            if (lc == 0 && sp + 2 <= STK::cap) push_children(nd, dneg, stk, sp);
+        }
+        if (lc == 0) break;
+        if (second)
+            leaf_items(S, la, lc, entry_local_ray<true>(e1, r), t_min, h, fc);
+        else
+            leaf_items(S, la, lc, r, t_min, h, fc);
+    }
+    hb = h;
+    if (h.prim == hg.prim) hb.prim = -1;  // e1 holds nothing that beats e0's winner
+    h = hg;
+}
+
 // (called with wave-uniform entries only: the media walk)
 template <int F, class STK>
 RTW_D void group_closest(const scene& S, const entry_v& e, const ray& r, double t_min, hit_state& h, STK& stk) {
@@ -2013,11 +2075,16 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
 #else
             volatile double* const cache = nullptr;
 #endif
+            hit_state hb{in_place<kDblMaxBits>(), -1, false};  // the fused walk's result for fuse_entry
             for (int k = 0; k < S.n_media; ++k) {
                 const int visit = ld(&S.media[k]);
                 const int ei = visit & kVisitEntry;
                 const entry_v e = view_entry<true>(S, ei);
-                if (e.kind == RTW_ENTRY_MEDIUM) {
+                if (RTW_FUSE_GROUPS && (F & F_GBVH) && (visit & kVisitFuse)) {
+                    fused_group_bvh(S, e, view_entry<true>(S, S.fuse_entry), r, kTMin, h, hb, stk);
+                } else if (RTW_FUSE_GROUPS && (F & F_GBVH) && (visit & kVisitMerge)) {
+                    if (hb.prim != -1 && better(hb.t, hb.prim, hb.rect, h.t, h.prim, h.rect, h.prim != -1)) h = hb;
+                } else if (e.kind == RTW_ENTRY_MEDIUM) {
                     double t;
                     if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk, visit, cache)) {
                         h.t = t;

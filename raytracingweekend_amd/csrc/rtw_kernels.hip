@@ -2406,6 +2406,31 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             dnodes16.clear();
         }
     }
+    // Fused group walks (rtw_device.h fused_group_bvh): the first group-BVH
+    // visit of the media walk whose group has no transforms, and the next
+    // group-BVH visit after it, are walked in one loop; each visited once.
+    int fuse_entry = -1;
+    if (RTW_FUSE_GROUPS && bvh_ok && !media.empty()) {
+        std::map<int, int> count;
+        for (int32_t v : media) ++count[v & kVisitEntry];
+        auto gbvh = [&](int e) {
+            return d->entries[e].kind == RTW_ENTRY_GROUP && dentries[e].bvh_root >= 0 && count[e] == 1;
+        };
+        int i0 = -1;
+        for (size_t i = 0; i < media.size() && i0 < 0; ++i) {
+            const int e = media[i] & kVisitEntry;
+            if (gbvh(e) && d->entries[e].n_ops == 0) i0 = (int)i;
+        }
+        for (size_t i = i0 + 1; i0 >= 0 && i < media.size(); ++i) {
+            const int e = media[i] & kVisitEntry;
+            if (gbvh(e)) {
+                fuse_entry = e;
+                media[i0] |= kVisitFuse;
+                media[i] |= kVisitMerge;
+                break;
+            }
+        }
+    }
     // device entries (dev_entry) and their op pool
     std::vector<dev_entry> dev_entries(std::max<size_t>(dentries.size(), 1));
     std::vector<dev_op> dev_ops;
@@ -2478,6 +2503,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.nodes = (const node_store*)at(11);
     S.bvh_bound = bvh_bound;
     S.node_scale = node_scale;
+    S.fuse_entry = fuse_entry;
     S.items = (const int32_t*)at(12);
     S.runs = (const world_run*)at(13);
     S.ysph = (const float*)at(14);
