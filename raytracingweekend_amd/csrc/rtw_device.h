@@ -1745,14 +1745,20 @@ RTW_D void group_bvh(const scene& S, int root, int root4, const ray& r, double t
 // (a deterministic group: no draws; its nodes are culled only against a t
 // that bounds what could still win).
 #ifndef RTW_FUSE_GROUPS
-#define RTW_FUSE_GROUPS 1
+#define RTW_FUSE_GROUPS 0
 #endif
+// (fuse false: e0's walk alone -- the media walk's one group-BVH walk site)
 template <class STK>
-RTW_D void fused_group_bvh(const scene& S, const entry_v& e0, const entry_v& e1, const ray& r, double t_min,
-                           hit_state& h, hit_state& hb, STK& stk) {
+RTW_D void fused_group_bvh(const scene& S, const entry_v& e0, const entry_v& e1, bool fuse, const ray& r,
+                           double t_min, hit_state& h, hit_state& hb, STK& stk) {
     const float t0 = t_lo32(t_min);
-    slab_ray sr = make_slab_ray(S, r);
-    int dneg = dir_mask(r.d);
+    slab_ray sr;
+    int dneg;
+    {
+        const ray r0 = entry_local_ray<true>(e0, r);
+        sr = make_slab_ray(S, r0);
+        dneg = dir_mask(r0.d);
+    }
     double fc = motion_frac(S, r.t, e0.movers);
     int sp = 0;
     stk.at(sp++) = e0.bvh_root;
@@ -1760,29 +1766,27 @@ RTW_D void fused_group_bvh(const scene& S, const entry_v& e0, const entry_v& e1,
     hit_state hg = h;
     for (;;) {
         int la = 0, lc = 0;
-        while (lc == 0) {
-            if (sp == 0) {
-                if (second) break;
-                second = true;  // e0 done: its winner bounds e1's walk
-                hg = h;
-                const ray r1 = entry_local_ray<true>(e1, r);
-                sr = make_slab_ray(S, r1);
-                dneg = dir_mask(r1.d);
-                fc = motion_frac(S, r.t, e1.movers);
-                stk.at(sp++) = e1.bvh_root;
-            }
+        while (lc == 0 && sp > 0) {  // group_bvh's inner loop, unchanged
             const bvh_node32 nd = node_at(S, stk.at(--sp));
             if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
             lc = node_count(nd);
             la = nd.a;
             if (lc == 0 && sp + 2 <= STK::cap) push_children(nd, dneg, stk, sp);
         }
-        if (lc == 0) break;
-        if (second)
-            leaf_items(S, la, lc, entry_local_ray<true>(e1, r), t_min, h, fc);
-        else
-            leaf_items(S, la, lc, r, t_min, h, fc);
+        if (lc == 0) {
+            if (second || !fuse) break;
+            second = true;  // e0 done: its winner bounds e1's walk
+            hg = h;
+            const ray r1 = entry_local_ray<true>(e1, r);
+            sr = make_slab_ray(S, r1);
+            dneg = dir_mask(r1.d);
+            fc = motion_frac(S, r.t, e1.movers);
+            stk.at(sp++) = e1.bvh_root;
+            continue;
+        }
+        leaf_items(S, la, lc, entry_local_ray<true>(second ? e1 : e0, r), t_min, h, fc);
     }
+    if (!fuse) return;
     hb = h;
     if (h.prim == hg.prim) hb.prim = -1;  // e1 holds nothing that beats e0's winner
     h = hg;
@@ -2080,8 +2084,12 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                 const int visit = ld(&S.media[k]);
                 const int ei = visit & kVisitEntry;
                 const entry_v e = view_entry<true>(S, ei);
-                if (RTW_FUSE_GROUPS && (F & F_GBVH) && (visit & kVisitFuse)) {
-                    fused_group_bvh(S, e, view_entry<true>(S, S.fuse_entry), r, kTMin, h, hb, stk);
+                if (RTW_FUSE_GROUPS && (F & F_GBVH) && e.kind != RTW_ENTRY_MEDIUM && e.bvh_root >= 0 &&
+                    !(visit & kVisitMerge)) {
+                    // every group-BVH walk of the media walk, fused or not, at one site
+                    const bool fuse = (visit & kVisitFuse) != 0;
+                    fused_group_bvh(S, e, view_entry<true>(S, fuse ? S.fuse_entry : ei), fuse, r, kTMin, h, hb,
+                                    stk);
                 } else if (RTW_FUSE_GROUPS && (F & F_GBVH) && (visit & kVisitMerge)) {
                     if (hb.prim != -1 && better(hb.t, hb.prim, hb.rect, h.t, h.prim, h.rect, h.prim != -1)) h = hb;
                 } else if (e.kind == RTW_ENTRY_MEDIUM) {
@@ -2093,7 +2101,10 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                     }
                 } else {
                     const ray lr = entry_local_ray<true>(e, r);
-                    group_closest<F>(S, e, lr, kTMin, h, stk);
+                    if (RTW_FUSE_GROUPS && (F & F_GBVH))  // group BVHs took the branch above
+                        group_scan(S, e.first_prim, e.n_prims, lr, kTMin, h, e.movers);
+                    else
+                        group_closest<F>(S, e, lr, kTMin, h, stk);
                 }
 #ifdef RTW_PROF_WALK
                 if (pw) {
