@@ -103,7 +103,28 @@ RTW_HD d3 operator+(d3 a, d3 b) { return d3{a.x + b.x, a.y + b.y, a.z + b.z}; }
 RTW_HD d3 operator-(d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 RTW_HD d3 operator*(d3 a, d3 b) { return d3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 RTW_HD d3 operator*(d3 a, double s) { return d3{a.x * s, a.y * s, a.z * s}; }
-RTW_HD d3 operator/(d3 a, double s) { return d3{a.x / s, a.y / s, a.z / s}; }
+// d3 / double (vec3.h operator/): on the device the three quotients share one
+// reciprocal (rtw_div.h rcp_hw / div_hw, bit for bit the compiler's own a / b
+// when |s| is in [2^-200, 2^200] and each |a| in [2^-800, 2^100]; a zero
+// numerator takes q = a * y, which carries division's sign rule); a wave
+// with a lane outside the range divides exactly.
+#ifndef RTW_DIV3_SHARED
+#define RTW_DIV3_SHARED 1
+#endif
+RTW_HD d3 operator/(d3 a, double s) {
+#if defined(__HIP_DEVICE_COMPILE__) && RTW_DIV3_SHARED
+    const bool ok = div_hw_ok_b_exp(s) && div_hw_ok_a0_exp(a.x) && div_hw_ok_a0_exp(a.y) && div_hw_ok_a0_exp(a.z);
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {  // wave-uniform: no divergent branch
+        const double y = rcp_hw(s);
+        auto q = [&](double v) {
+            const double q0 = v * y;
+            return v == 0.0 ? q0 : div_hw(v, s, y);
+        };
+        return d3{q(a.x), q(a.y), q(a.z)};
+    }
+#endif
+    return d3{a.x / s, a.y / s, a.z / s};
+}
 RTW_HD d3 operator-(d3 a) { return d3{-a.x, -a.y, -a.z}; }
 RTW_HD double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RTW_HD double len2(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }

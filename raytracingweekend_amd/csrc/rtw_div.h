@@ -82,6 +82,14 @@ __device__ __forceinline__ bool div_hw_ok_a(double a) {
     const double m = __builtin_fabs(a);
     return m >= 0x1p-800 && m <= 0x1p100;
 }
+// The same ranges (slightly narrower at the top: |b| < 2^200, |a| < 2^100)
+// from the biased exponent in the high word: 32-bit integer work, no 64-bit
+// constants to hold in registers.  div_hw_ok_a0 also admits a zero numerator.
+__device__ __forceinline__ uint32_t exp_bits(double v) {
+    return ((uint32_t)(__builtin_bit_cast(unsigned long long, v) >> 52)) & 0x7ffu;
+}
+__device__ __forceinline__ bool div_hw_ok_b_exp(double b) { return exp_bits(b) - 823u < 400u; }
+__device__ __forceinline__ bool div_hw_ok_a0_exp(double a) { return a == 0.0 || exp_bits(a) - 223u < 900u; }
 #endif
 
 }  // namespace rtwd
