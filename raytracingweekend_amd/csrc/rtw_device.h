@@ -39,6 +39,14 @@ constexpr double kInvPi = 1.0 / kPi;
 #ifndef RTW_RADIANCE_FAST
 #define RTW_RADIANCE_FAST 1
 #endif
+// ... and (RTW_RADIANCE_RCP) the remaining radiance-only quotients -- the
+// lambertian factor, the rect light's pdf, the sphere light's 1 / solid angle -- as
+// products with rcp_hw's reciprocal (within an ulp of 1 / x; a wave with a
+// lane outside [2^-200, 2^200] divides exactly, so zeros and infinities keep
+// division's results).
+#ifndef RTW_RADIANCE_RCP
+#define RTW_RADIANCE_RCP 0
+#endif
 constexpr double kDblMax = 1.7976931348623157e308; // std::numeric_limits<double>::max()
 constexpr double kFltMax = 3.4028234663852886e38;  // FLT_MAX widened
 constexpr double kTMin = (double)0.001f;           // RayTracingWeekend.cpp:52 (float literal)
@@ -108,8 +116,12 @@ RTW_HD d3 operator*(d3 a, double s) { return d3{a.x * s, a.y * s, a.z * s}; }
 // when |s| is in [2^-200, 2^200] and each |a| in [2^-800, 2^100]; a zero
 // numerator takes q = a * y, which carries division's sign rule); a wave
 // with a lane outside the range divides exactly.
+// Measured (1 MI355X, A/B, profiles/r04/ab_div3_r4m.log; GPU suite green
+// with it): T 4 293 vs 4 440, C2 -0.7 %, C3 -2.6 %, C5 -2.5 % -- the range
+// checks, the wave vote and two more spilled VGPRs cost more than the two
+// hardware division sequences they replace.  Off.
 #ifndef RTW_DIV3_SHARED
-#define RTW_DIV3_SHARED 1
+#define RTW_DIV3_SHARED 0
 #endif
 RTW_HD d3 operator/(d3 a, double s) {
 #if defined(__HIP_DEVICE_COMPILE__) && RTW_DIV3_SHARED
@@ -126,6 +138,13 @@ RTW_HD d3 operator/(d3 a, double s) {
     return d3{a.x / s, a.y / s, a.z / s};
 }
 RTW_HD d3 operator-(d3 a) { return d3{-a.x, -a.y, -a.z}; }
+// a / b for a quantity that only scales radiance (RTW_RADIANCE_RCP)
+__device__ __forceinline__ double rad_div(double a, double b) {
+#if RTW_RADIANCE_RCP
+    if (__builtin_amdgcn_ballot_w64(!div_hw_ok_b_exp(b)) == 0) return a * rcp_hw(b);
+#endif
+    return a / b;
+}
 RTW_HD double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RTW_HD double len2(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
 RTW_HD double len(d3 a) { return __builtin_sqrt(len2(a)); }
@@ -2270,7 +2289,7 @@ RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
         const double distance_squared = t * t * len2(v);
 #if RTW_RADIANCE_FAST
         // |dot(v, n)| / |v| folded into one quotient (v.y != 0: the rect was hit)
-        return distance_squared * len(v) / (fabs(v.y) * area);
+        return rad_div(distance_squared * len(v), fabs(v.y) * area);
 #else
         const double cosine = fabs(dot(v, d3{0, 1, 0}) / len(v));
         return distance_squared / (cosine * area);
@@ -2283,9 +2302,17 @@ RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
         // (STATIC: no moving spheres, the fraction is never read)
         if (!sphere_t(q, r, 0.001, __builtin_inf(), t, STATIC ? 0.0 : motion_frac(S, r.t, q.type >= DP_MOVING_COMMON)))
             return 0.0;
+#if RTW_RADIANCE_FAST
+        // (magnitude only: the pdf's sign is that of the hit above; r^2 / d^2
+        // stays a division, so 1 - r^2 / d^2 rounds as the reference's does
+        // next to the sphere, where it cancels)
+        const double cos_theta_max = __builtin_sqrt(1 - q.p[9] / len2(ld3(q.p) - o));
+        return rad_div(1.0, kTwoPi * (1.0 - cos_theta_max));
+#else
         const double cos_theta_max = __builtin_sqrt(1 - q.p[9] / len2(ld3(q.p) - o));  // p[9] = radius * radius
         const double solid_angle = kTwoPi * (1.0 - cos_theta_max);
         return 1.0 / solid_angle;
+#endif
     }
     return 0.0;  // hittable.h:36
 }

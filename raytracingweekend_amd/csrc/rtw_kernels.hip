@@ -489,7 +489,7 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
         // draws nothing, and a late read keeps it out of the busiest registers
 #if RTW_RADIANCE_FAST
         // attenuation * scattering_pdf / pdf_val as one scalar quotient
-        const double w = cosine < 0 ? 0 : cosine / (kPi * pdf_val);
+        const double w = cosine < 0 ? 0 : rad_div(cosine, kPi * pdf_val);
         return scatter(texture_value<M>(S, m.texture, p) * w, p, dir);
 #else
         const double spdf = cosine < 0 ? 0 : cosine / kPi;
