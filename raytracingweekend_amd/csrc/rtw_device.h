@@ -173,13 +173,18 @@ RTW_D uint32_t mr_next(uint32_t& s) {
 }
 
 // libstdc++ generate_canonical<double,53>(minstd_rand): two raw draws.
-RTW_D double canon(uint32_t& s) {
-    const double e1 = (double)(mr_next(s) - 1u);
-    const double e2 = (double)(mr_next(s) - 1u);
+RTW_D double canon_raw(uint32_t r1, uint32_t r2) {
+    const double e1 = (double)(r1 - 1u);
+    const double e2 = (double)(r2 - 1u);
     double sum = 0.0 + e1 * 1.0;
     sum = sum + e2 * kCanonR;
     double r = div_rcp(sum, kCanonDiv, kCanonRcp);  // sum in [0, 2^62]: always in the guard
     return r >= 1.0 ? kOneMinusUlp : r;
+}
+RTW_D double canon(uint32_t& s) {
+    const uint32_t r1 = mr_next(s);
+    const uint32_t r2 = mr_next(s);
+    return canon_raw(r1, r2);
 }
 RTW_D double rnd01(uint32_t& s) { return canon(s) * (1.0 - 0.0) + 0.0; }
 RTW_D double rnd(uint32_t& s, double a, double b) { return a + (b - a) * rnd01(s); }  // utility.h:14-20
@@ -202,7 +207,42 @@ RTW_D int random_int(uint32_t& s, int a, int b) {  // utility.h:22-25
 }
 
 // utility.h:27-35 — vec3(U, U, U) is built right to left by g++: z, y, x.
+// The rejection loop decided in fp32 (RTW_RIUS_FP32): a wave runs its
+// longest lane's number of tries (~4 for the metal lanes of a random_balls
+// wave, ~6 for the isotropic lanes of a Book-2 wave), so each try draws its
+// six raw values and tests 2 (e2 / R) - 1 -- the canonical draw's leading
+// term, within 2^-22.4 of it -- in fp32: |d32 - d| < 2^-18 for d = |p|^2, so
+// d32 < 1 - 2^-14 accepts and d32 >= 1 + 2^-14 rejects exactly as the fp64
+// test would, and a try in between takes the fp64 test.  The accepted try's
+// p is then formed from its raw draws in fp64, once: the same draws, the
+// same value, the same engine state as the reference's loop.
+#ifndef RTW_RIUS_FP32
+#define RTW_RIUS_FP32 1
+#endif
 RTW_D d3 random_in_unit_sphere(uint32_t& s) {
+#if RTW_RIUS_FP32
+    constexpr float k2Rf = (float)(2.0 / kCanonR);  // 2 / R rounded
+    auto lead = [&](uint32_t raw) { return __builtin_fmaf((float)(raw - 1u), k2Rf, -1.0f); };
+    auto exact = [&](uint32_t z1, uint32_t z2, uint32_t y1, uint32_t y2, uint32_t x1, uint32_t x2) {
+        const double z = canon_raw(z1, z2) * (1.0 - 0.0) + 0.0;
+        const double y = canon_raw(y1, y2) * (1.0 - 0.0) + 0.0;
+        const double x = canon_raw(x1, x2) * (1.0 - 0.0) + 0.0;
+        return d3{x, y, z} * 2.0 - d3{1.0, 1.0, 1.0};
+    };
+    uint32_t z1, z2, y1, y2, x1, x2;
+    for (;;) {
+        z1 = mr_next(s), z2 = mr_next(s);
+        y1 = mr_next(s), y2 = mr_next(s);
+        x1 = mr_next(s), x2 = mr_next(s);
+        const float px = lead(x2), py = lead(y2), pz = lead(z2);
+        const float d32 = __builtin_fmaf(px, px, __builtin_fmaf(py, py, pz * pz));
+        if (d32 < 1.0f - 0x1p-14f) break;
+        if (!(d32 < 1.0f + 0x1p-14f)) continue;
+        const d3 q = exact(z1, z2, y1, y2, x1, x2);
+        if (dot(q, q) < 1.0) break;
+    }
+    return exact(z1, z2, y1, y2, x1, x2);
+#else
     d3 p;
     do {
         const double z = rnd01(s);
@@ -211,6 +251,7 @@ RTW_D d3 random_in_unit_sphere(uint32_t& s) {
         p = d3{x, y, z} * 2.0 - d3{1.0, 1.0, 1.0};
     } while (dot(p, p) >= 1.0);
     return p;
+#endif
 }
 
 RTW_D d3 random_cosine_direction(uint32_t& s) {  // utility.h:54-67
@@ -2421,13 +2462,41 @@ RTW_D double schlick_r0(double cosine, double r0) { return r0 + (1 - r0) * pow5(
 
 // ------------------------------------------------------------------ camera
 // camera::get_ray camera.h:36-50, random_in_unit_disk :61-69 (y drawn first)
+// (RTW_DISK_FP32: the rejection loop decided in fp32 as random_in_unit_sphere's)
+#ifndef RTW_DISK_FP32
+#define RTW_DISK_FP32 RTW_RIUS_FP32
+#endif
 RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng) {
     d3 p;
+#if RTW_DISK_FP32
+    {
+        constexpr float k2Rf = (float)(2.0 / kCanonR);
+        auto lead = [&](uint32_t raw) { return __builtin_fmaf((float)(raw - 1u), k2Rf, -1.0f); };
+        auto exact = [&](uint32_t y1, uint32_t y2, uint32_t x1, uint32_t x2) {
+            const double y = canon_raw(y1, y2) * (1.0 - 0.0) + 0.0;
+            const double x = canon_raw(x1, x2) * (1.0 - 0.0) + 0.0;
+            return d3{x, y, 0} * 2.0 - d3{1, 1, 0};
+        };
+        uint32_t y1, y2, x1, x2;
+        for (;;) {
+            y1 = mr_next(rng), y2 = mr_next(rng);
+            x1 = mr_next(rng), x2 = mr_next(rng);
+            const float px = lead(x2), py = lead(y2);
+            const float d32 = __builtin_fmaf(px, px, py * py);
+            if (d32 < 1.0f - 0x1p-14f) break;
+            if (!(d32 < 1.0f + 0x1p-14f)) continue;
+            const d3 q = exact(y1, y2, x1, x2);
+            if (dot(q, q) < 1.0) break;
+        }
+        p = exact(y1, y2, x1, x2);
+    }
+#else
     do {
         const double y = rnd01(rng);
         const double x = rnd01(rng);
         p = d3{x, y, 0} * 2.0 - d3{1, 1, 0};
     } while (dot(p, p) >= 1.0);
+#endif
     const d3 rd = p * c.lens_radius;
     const d3 offset = ld3(c.u) * rd.x + ld3(c.v) * rd.y;
     const double time = c.time0 + rnd01(rng) * (c.time1 - c.time0);
