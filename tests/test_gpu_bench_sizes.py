@@ -7,7 +7,8 @@ far too slow for whole images at those sizes, but every pixel is independent,
 so the kernels are checked on BANDS of the full-size images: a few rows spread
 over the image (row_begin / row_step of rtw_render_params) and the LAST samples
 of the pixel's range (the top of the key space), against the oracle on the
-same rows and samples.  Tolerance as tests/test_gpu_parity.py: 1e-4 per
+same rows and samples -- and, for T, C2 and C3, on the WHOLE full-size image
+at the last sample of every pixel.  Tolerance as tests/test_gpu_parity.py: 1e-4 per
 canvas channel (north star), equal device-counted traversals.
 """
 import numpy as np
@@ -72,6 +73,39 @@ def test_band_matches_oracle(gpu, name, scene, nx, ny, spp, cnt, bvh, rows):
     d = np.abs(finalize_np(acc[sel], cnt) - finalize_np(ref[sel], cnt))
     assert np.all(np.isfinite(acc[sel]))
     assert d.max() <= TOL, f"{name}: max per-channel diff {d.max()}"
+
+
+# whole images at the bench resolution, the LAST sample of each pixel (the
+# oracle renders them in seconds; Book 2's 2.56 M paths would take minutes)
+WHOLE = [
+    ("T", "cornell_box", 800, 800, 1024, False),
+    ("C2", "random_balls", 1200, 800, 256, False),
+    ("C3", "random_balls", 1200, 800, 1024, True),
+]
+
+
+@pytest.mark.parametrize("name,scene,nx,ny,spp,bvh", WHOLE, ids=[w[0] for w in WHOLE])
+def test_whole_image_last_sample_matches_oracle(gpu, name, scene, nx, ny, spp, bvh):
+    """Every pixel of the full-size image (not a band), at the top of the
+    sample range: equal device-counted traversals, canvas within 1e-4, and
+    the quantised (PPM) channels equal except at rounding boundaries."""
+    depth, seed = 50, 0
+    sd = gpu.SceneDesc(scene, nx / ny, use_bvh=bvh)
+    ds = gpu.DeviceScene(sd)
+    try:
+        acc, st = ds.render_accumulate(nx, ny, spp, depth, seed, spp_begin=spp - 1, spp_count=1)
+    finally:
+        ds.close()
+    ref, seg = oracle_sums(gpu.SceneDesc(scene, nx / ny), nx, ny, spp, depth, seed, spp_begin=spp - 1, spp_count=1)
+    assert st["samples"] == nx * ny
+    assert st["segments"] == seg, "device-counted traversals differ from the oracle's"
+    c_gpu, c_ref = finalize_np(acc, 1), finalize_np(ref, 1)
+    assert np.all(np.isfinite(c_gpu))
+    d = np.abs(c_gpu - c_ref)
+    assert d.max() <= TOL, f"{name}: max per-channel diff {d.max()}"
+    q_gpu = (np.float64(np.float32(255.99)) * c_gpu).astype(np.int64)
+    q_ref = (np.float64(np.float32(255.99)) * c_ref).astype(np.int64)
+    assert (q_gpu != q_ref).sum() <= max(1, d.size // 10000)
 
 
 def test_multi_pass_at_T_resolution(gpu, monkeypatch):
