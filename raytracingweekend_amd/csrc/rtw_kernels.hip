@@ -1339,15 +1339,25 @@ constexpr int FF_NONOISE = 1 << 12;
 #ifndef RTW_FAST_BVH_WAVES
 #define RTW_FAST_BVH_WAVES 8
 #endif
+// HOME (RTW_FAST_HOME(F)): the path's throughput and sample id wait in the
+// lane's LDS home slots instead of registers (k_persist's plan), and the
+// segments are counted per wave in a scalar register -- the loop-carried
+// values the media kernel (F_MEDIA) spilled to scratch at 8 waves / 64 VGPRs.
+#ifndef RTW_FAST_HOME
+#define RTW_FAST_HOME(F) 0
+#endif
 template <int F, bool LST>
 __global__ __launch_bounds__(rtwf::kFastBlock) __attribute__((amdgpu_waves_per_eu(RTW_FAST_BVH_WAVES)))
 void k_fast(fast_args) {
     using namespace rtwf;
     constexpr bool NOISE = (F & FF_NONOISE) == 0;
+    constexpr bool HOME = RTW_FAST_HOME(F) != 0;
     constexpr int kFW = kFastBlock / 64;
     extern __shared__ __attribute__((aligned(16))) char s_nodes[];
     __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kFastBlock];
     __shared__ uint32_t s_cnt[kFW];
+    __shared__ float s_thr[HOME ? 3 : 1][HOME ? kFastBlock : 1];
+    __shared__ uint32_t s_q[HOME ? kFastBlock : 1];
     if (LST) {  // the BVH node packet (the top levels of every tree)
         const fast_args& A = fast_args_now();
         const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
@@ -1361,8 +1371,13 @@ void k_fast(fast_args) {
     fray r{f3{0, 0, 0}, f3{0, 0, 1}, 0};
     f3 thr{1, 1, 1};
     uint32_t rng = 0, depth = 0, q = 0, segs = 0;
+    uint32_t wsegs = 0;  // HOME: the wave's segments (wave-uniform)
     bool open = true;  // wave-uniform: the queue may still hold samples
     for (;;) {
+        // (HOME: an opaque copy of the thread index forms the slot addresses
+        // where they are used, as in k_persist)
+        uint32_t tid = threadIdx.x;
+        if constexpr (HOME) asm volatile("" : "+v"(tid));
         // idle lanes take new camera samples (RayTracingWeekend.cpp:227-231)
         const bool idle = depth == 0;
         const unsigned long long m = __ballot(idle);
@@ -1399,9 +1414,14 @@ void k_fast(fast_args) {
                 const float u = ((float)i + u01(rng)) * rcp((float)A.J.nx);
                 const float v = ((float)j + u01(rng)) * rcp((float)A.J.ny);
                 r = camera_ray(A.cam, u, v, rng);
-                thr = f3{1, 1, 1};
+                if constexpr (HOME) {
+                    s_thr[0][tid] = 1.0f, s_thr[1][tid] = 1.0f, s_thr[2][tid] = 1.0f;
+                    s_q[tid] = nq;
+                } else {
+                    thr = f3{1, 1, 1};
+                    q = nq;
+                }
                 depth = (uint32_t)A.J.max_depth;
-                q = nq;
             }
         }
         if (!__any(depth != 0)) break;
@@ -1418,25 +1438,48 @@ void k_fast(fast_args) {
             priv_stackf stk;
             h = world_closest<F>(fast_args_now().S, r, rng, stk);
         }
-        ++segs;
+        if constexpr (HOME)
+            wsegs += (uint32_t)__popcll(__ballot(true));
+        else
+            ++segs;
         // one segment of color() (RayTracingWeekend.cpp:52-159)
         const seg_f sg = shade<NOISE>(fast_args_now().S, r, h, rng, depth);
         bool end = !sg.cont;
         f3 L{0, 0, 0};
-        if (sg.cont) {
-            thr = thr * sg.w;
-            r = sg.next;
-            --depth;
+        if constexpr (HOME) {
+            uint32_t me = threadIdx.x;
+            asm volatile("" : "+v"(me));
+            const f3 t{s_thr[0][me], s_thr[1][me], s_thr[2][me]};
+            if (sg.cont) {
+                const f3 n = t * sg.w;
+                s_thr[0][me] = n.x, s_thr[1][me] = n.y, s_thr[2][me] = n.z;
+                r = sg.next;
+                --depth;
+            } else {
+                L = t * sg.w;
+                store_record_f32(fast_args_now().J.L, s_q[me], L.x, L.y, L.z);
+                depth = 0;
+            }
         } else {
-            L = thr * sg.w;
-        }
-        if (end) {
-            store_record_f32(fast_args_now().J.L, q, L.x, L.y, L.z);
-            depth = 0;
+            if (sg.cont) {
+                thr = thr * sg.w;
+                r = sg.next;
+                --depth;
+            } else {
+                L = thr * sg.w;
+            }
+            if (end) {
+                store_record_f32(fast_args_now().J.L, q, L.x, L.y, L.z);
+                depth = 0;
+            }
         }
     }
-    for (int off = 32; off > 0; off >>= 1) segs += __shfl_down(segs, off, 64);
-    if (lane == 0) s_cnt[threadIdx.x >> 6] = segs;
+    if constexpr (HOME) {
+        if (lane == 0) s_cnt[threadIdx.x >> 6] = wsegs;
+    } else {
+        for (int off = 32; off > 0; off >>= 1) segs += __shfl_down(segs, off, 64);
+        if (lane == 0) s_cnt[threadIdx.x >> 6] = segs;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
@@ -3025,9 +3068,13 @@ int lst_stack_need(const handle_t* h) { return RTW_BVH4 ? h->stack4_need : h->st
 void launch_fast(bool probe, const handle_t* h, hipStream_t st, const fast_args& A, std::string* name = nullptr) {
     const int f = h->features & (F_MEDIA | F_WBVH | F_GBVH);
 #ifdef RTW_SUBSET_FAST  // experiment builds (scripts/ru_kernel.sh): the list scenes' fp32 kernel only
+#ifdef RTW_SUBSET_FAST_F  // ... or one BVH kernel k_fast<RTW_SUBSET_FAST_F, true>
+    launch_fast_t<RTW_SUBSET_FAST_F, true>(probe, name, h->cus, st, A);
+#else
     launch_fast_sort_t<FF_NONOISE, true>(probe, name, h->cus, st, A, static_cast<const char*>(h->scene32.p),
                                          h->f32_bytes);
     launch_fast_t<F_WBVH | FF_NONOISE, true>(probe, name, h->cus, st, A);
+#endif
 #else
     if ((f & (F_WBVH | F_GBVH)) == 0 && fast_sort_enabled()) {  // list scenes: regrouping kernel
         const char* base = static_cast<const char*>(h->scene32.p);

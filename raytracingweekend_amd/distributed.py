@@ -41,8 +41,11 @@ def _world(group):
     return dist.get_world_size(group), dist.get_rank(group)
 
 
+PHASES = ("render", "reduce", "finalize")
+
+
 def render_step(render_fn: Callable, finalize_fn: Optional[Callable], accum, canvas, nx: int, ny: int, spp: int, *,
-                mode: str = "spp", group=None):
+                mode: str = "spp", group=None, timings: Optional[dict] = None, sync: Optional[Callable] = None):
     """One render of the whole image by every rank of `group`:
 
       accum <- 0; render_fn(spp_begin, spp_count, row_begin, row_step, accum)
@@ -50,11 +53,26 @@ def render_step(render_fn: Callable, finalize_fn: Optional[Callable], accum, can
       on rank 0 finalize_fn(accum, canvas) writes min(sqrt(accum / spp), 1)
       (RayTracingWeekend.cpp:241-244).
 
+    timings: when given, the wall milliseconds of this rank's phases are
+    ADDED into it under PHASES ("render": zero + render, "reduce": the
+    collective, "finalize"), each closed by `sync()` (torch.cuda.synchronize
+    on a GPU) so that queued device work is counted in its own phase.
+
     Returns render_fn's result on this rank (its stats), or None when the
     rank had no shard."""
+    import time
+
     import torch.distributed as dist
 
     world, rank = _world(group)
+    t = [time.perf_counter()]
+
+    def mark():
+        if timings is not None:
+            if sync is not None:
+                sync()
+            t.append(time.perf_counter())
+
     accum.zero_()
     out = None
     if mode == "spp":
@@ -66,10 +84,16 @@ def render_step(render_fn: Callable, finalize_fn: Optional[Callable], accum, can
             out = render_fn(0, spp, rank, world, accum)
     else:
         raise ValueError(f"unknown sharding mode {mode!r}")
+    mark()
     if world > 1:
         dist.reduce(accum, dst=0, group=group)
+    mark()
     if rank == 0 and finalize_fn is not None:
         finalize_fn(accum, canvas)
+    mark()
+    if timings is not None:
+        for k, name in enumerate(PHASES):
+            timings[name] = timings.get(name, 0.0) + (t[k + 1] - t[k]) * 1e3
     return out
 
 

@@ -203,3 +203,14 @@ def test_cpu_baseline_port_is_one_threaded_call(bench, monkeypatch, built):
         rowwise += r
         segs += s
     assert seg == segs and np.array_equal(strided, rowwise)
+
+
+def test_bench_line_drops_an_unbounded_valu_figure(bench):
+    """In the bench line a VALU fraction above 1 (a slightly stale PMC
+    record) is dropped with a warning instead of aborting the run before the
+    line is printed; roofline() itself keeps refusing it."""
+    out = {"frac": 0.2, "valu": {"class_weighted": {"frac": 1.3}}}
+    got = bench.bounded_valu(out)
+    assert "valu" not in got and "not a roofline fraction" in got["warning"] and got["frac"] == 0.2
+    ok = {"frac": 0.2, "valu": {"class_weighted": {"frac": 0.7}}}
+    assert bench.bounded_valu(dict(ok)) == ok

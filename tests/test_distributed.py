@@ -50,6 +50,38 @@ def _worker(rank, world, port, mode, q):
     from raytracingweekend_amd.render import SceneDesc
     sd = SceneDesc("cornell_box", NX / NY)
     accum = torch.zeros(NX * NY * 3, dtype=torch.float64)
+    if mode == "phases":
+        # bench.py's timed step: render_step's per-rank phase times, reduced
+        # over the ranks by bench.rank_phases and put into the rank-0 line
+        import bench
+        from oracle_lib import finalize_np
+        canvas_t = torch.zeros(NX * NY * 3, dtype=torch.float64)
+        ms = {}
+
+        def fin(acc, canvas):
+            canvas.copy_(torch.from_numpy(finalize_np(acc.numpy(), SPP)))
+
+        fn = _oracle_fn(sd)
+        stats = {"samples": 0}
+
+        def counting(b, c, r0, rs, acc):
+            fn(b, c, r0, rs, acc)
+            stats["samples"] += NX * NY * c
+
+        render_step(counting, fin, accum, canvas_t, NX, NY, SPP, timings=ms)
+        local = dict(ms, kernel=10.0 * (rank + 1))  # a stand-in kernel time per rank
+        phases = bench.rank_phases(local, world)
+        t = torch.tensor([float(stats["samples"])], dtype=torch.float64)
+        dist.all_reduce(t)
+        if rank == 0:
+            import sys as _s
+            _s.argv = ["bench.py", "--gpus", "2", "--steps", "1", "--scene", "cornell_box", "--nx", str(NX),
+                       "--ny", str(NY), "--spp", str(SPP)]
+            a = bench.parse()
+            line = bench.result_line(a, world, SPP, 0.5, float(t.item()), 1000.0, 1.0, None, phases)
+            q.put((line, ms))
+        dist.destroy_process_group()
+        return
     if mode == "step":
         # bench.py's step: render_step with a finalize into a canvas tensor
         from oracle_lib import finalize_np
@@ -101,3 +133,29 @@ def test_sample_range_partition():
             for b, c in got:
                 assert b == pos
                 pos += c
+
+
+def test_two_rank_line_carries_per_rank_phases(built):
+    """bench.py --gpus N: the rank-0 JSON line carries each phase's max / min
+    over the ranks and rank 0's value (all_reduce MAX / MIN, as the step time
+    is) -- the diagnosis of a slow rank, the reduce and the finalize in the
+    driver's N > 1 runs (round-4 verdict, next #8)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, "phases", q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    line, ms0 = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ph = line["rank_phases_ms"]
+    assert set(ph) == {"kernel", "render", "reduce", "finalize"}
+    assert ph["kernel"] == {"max": 20.0, "min": 10.0, "rank0": 10.0}
+    for k in ("render", "reduce", "finalize"):
+        assert ph[k]["max"] >= ph[k]["rank0"] >= ph[k]["min"] >= 0.0, (k, ph[k])
+        assert abs(ph[k]["rank0"] - round(ms0[k], 3)) < 1e-9, k
+    assert ph["render"]["min"] > 0.0  # both ranks rendered their shard
+    assert line["n_gpus"] == 2 and line["value"] == round(NX * NY * SPP / 0.5 / 1e6, 3)
+    assert line["config"]["parallelism"] == "spp-shard x2 + RCCL reduce"
