@@ -244,7 +244,9 @@ typedef struct rtw_render_params {
     int32_t row_step;      /* 0 or 1 = every row                                    */
     int32_t accum_on_device; /* 1: accum_rgb is device memory of this handle's GPU
                                 (hipMalloc / torch allocators) or managed memory
-                                (hipMallocManaged); anything else: RTW_ERR_INVALID */
+                                (hipMallocManaged; rtw_render_multi over several
+                                GPUs refuses it: RTW_ERR_UNSUPPORTED); anything
+                                else: RTW_ERR_INVALID */
     int32_t collect_kernel_times; /* 1: hipEvents around traversal launches,    */
                                   /* 2: and shade launches (adds queue gaps)   */
     int32_t wavefront_paths; /* paths in flight (0 = library default)             */

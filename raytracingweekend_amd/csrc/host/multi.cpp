@@ -121,7 +121,7 @@ extern "C" int rtw_render_multi(int ngpus, void* const* handles, const rtw_camer
     if (R.precision != RTW_PRECISION_FP64 && R.precision != RTW_PRECISION_FP32)
         return rtw_fail(RTW_ERR_INVALID, "rtw_render_multi: unknown precision");
     if (R.accum_on_device)
-        if (int rc = rtw_check_device_ptr(accum_root, devs[0], "rtw_render_multi")) return rc;
+        if (int rc = rtw_check_device_ptr(accum_root, devs[0], "rtw_render_multi", ngpus == 1)) return rc;
     const size_t elems = (size_t)R.nx * (size_t)R.ny * 3;
 
     std::lock_guard<std::mutex> lock(g_mu);  // one multi-render at a time per process

@@ -265,6 +265,11 @@ public:
     };
     std::vector<node> nodes;
     std::vector<int> order;
+    // some object holds a constant_medium (directly or through lists and
+    // transforms): hit() is then hittable_list::hit's double walk over every
+    // object -- a medium's draws depend on the t_max the list walk hands it
+    // (hittable.h:420-489), which a distance search would change
+    bool media = false;
 
 private:
     void build(double time0, double time1);

@@ -26,7 +26,11 @@ int validate_desc(const rtw_scene_desc* d);
 // the host library (multi.cpp); not part of the C ABI.
 int rtw_handle_device(void* handle);                                             // -1 for null
 int rtw_handle_add_device(void* handle, double* dst, const double* src, size_t n);  // dst += src, synchronous
-// RTW_OK when `p` is device memory of `device` (an accum_on_device pointer),
-// else RTW_ERR_INVALID naming `what`: a foreign pointer would be written by
-// kernels of another GPU (a fault, or silent peer writes).
-int rtw_check_device_ptr(const void* p, int device, const char* what);
+// RTW_OK when `p` is device memory of `device`, or (allow_managed) managed
+// memory (hipMallocManaged), as an accum_on_device pointer; else
+// RTW_ERR_INVALID naming `what`: a foreign pointer would be written by
+// kernels of another GPU (a fault, or silent peer writes).  Managed memory
+// is accepted where a one-GPU test covers it (rtw_render_accumulate, and
+// rtw_render_multi over one GPU); rtw_render_multi over several GPUs refuses
+// it (RTW_ERR_UNSUPPORTED) until a multi-GPU run covers the cross-device write.
+int rtw_check_device_ptr(const void* p, int device, const char* what, bool allow_managed = true);

@@ -190,7 +190,26 @@ bool slab_overlap(const aabb& b, const ray& r, double tmin, double tmax, double&
 }
 }  // namespace
 
+// does `h` hold a constant_medium (itself, or below lists, boxes, bvh_nodes
+// and transforms)?
+bool holds_medium(const hittable* h) {
+    if (!h) return false;
+    if (dynamic_cast<const constant_medium*>(h)) return true;
+    if (auto l = dynamic_cast<const hittable_list*>(h)) {
+        for (const auto& o : l->objects)
+            if (holds_medium(o.get())) return true;
+        return false;
+    }
+    if (auto b = dynamic_cast<const bvh_node*>(h)) return b->media;
+    if (auto f = dynamic_cast<const flip_normals*>(h)) return holds_medium(f->ptr.get());
+    if (auto t = dynamic_cast<const translate*>(h)) return holds_medium(t->ptr.get());
+    if (auto y = dynamic_cast<const rotate_y*>(h)) return holds_medium(y->ptr.get());
+    return false;
+}
+
 void bvh_node::build(double time0, double time1) {
+    media = false;
+    for (const auto& o : objects) media = media || holds_medium(o.get());
     // per object: its box over the shutter (an object without one is kept
     // in every leaf's candidate walk: the box of everything)
     const int n = (int)objects.size();
@@ -269,6 +288,23 @@ bvh_node::bvh_node(const std::vector<std::shared_ptr<hittable>>& l, double time0
 
 bool bvh_node::hit(const ray& r, double t_min, double t_max, hit_record& rec) const {
     if (objects.empty()) return false;
+    if (media) {
+        // hittable_list::hit (hittable_list.h:11-36): every object twice, in
+        // list order, each below the closest so far -- the media draw exactly
+        // as in the list (the distance search below would call a
+        // medium's hit with other bounds, or more often)
+        hit_record tmp;
+        bool found = false;
+        double bound = t_max;
+        for (int walk = 0; walk < 2; ++walk)
+            for (const auto& o : objects)
+                if (o->hit(r, t_min, bound, tmp)) {
+                    found = true;
+                    bound = tmp.t;
+                    rec = tmp;
+                }
+        return found;
+    }
     // 1. the closest distance: nearest-first walk, each object tested below
     //    the closest found so far (the set of hits below a bound does not
     //    depend on the order, so neither does its minimum)

@@ -3281,7 +3281,7 @@ int rtw_handle_add_device(void* handle, double* dst, const double* src, size_t n
 // allocators) or managed memory (hipMallocManaged: any GPU).  Host memory,
 // pinned host memory and unknown pointers are refused (a host pointer is
 // passed with accum_on_device = 0 instead).
-int rtw_check_device_ptr(const void* p, int device, const char* what) {
+int rtw_check_device_ptr(const void* p, int device, const char* what, bool allow_managed) {
     hipPointerAttribute_t a;
     std::memset(&a, 0, sizeof a);
     if (hipPointerGetAttributes(&a, p) != hipSuccess ||
@@ -3290,6 +3290,9 @@ int rtw_check_device_ptr(const void* p, int device, const char* what) {
         return rtw_fail(RTW_ERR_INVALID, std::string(what) + ": accum_on_device is set but the accumulator is not "
                                                               "device or managed memory");
     }
+    if (a.type == hipMemoryTypeManaged && !allow_managed)
+        return rtw_fail(RTW_ERR_UNSUPPORTED, std::string(what) + ": a managed-memory accumulator is supported with "
+                                                                  "one GPU only (the cross-device write is unverified)");
     if (a.type == hipMemoryTypeDevice && a.device != device)
         return rtw_fail(RTW_ERR_INVALID, std::string(what) + ": the device accumulator lives on device " +
                                              std::to_string(a.device) + ", the scene on device " +

@@ -53,13 +53,16 @@ def test_host_color_matches_reference_render(host_render, tmp_path, case):
 
 @pytest.mark.parametrize("scene,nx,ny,spp", [("random_balls", 48, 32, 2), ("cornell_box", 24, 24, 2),
                                              ("nested_plain", 24, 24, 2), ("dielectric", 32, 16, 2),
-                                             ("light_sample", 32, 16, 2)])
+                                             ("light_sample", 32, 16, 2), ("book2_final", 16, 16, 2),
+                                             ("nested", 24, 24, 2)])
 def test_host_bvh_equals_flat_list(host_render, tmp_path, scene, nx, ny, spp):
     """bvh_node::hit (median-split tree, nearest-first walk, then the list
     walk over the objects reaching the closest distance) picks the same
     record as hittable_list::hit on every path: identical sums and
-    traversals.  (Scenes with media are left out: a bvh_node over a medium
-    draws in another order, and the flattener refuses one.)"""
+    traversals.  A bvh_node holding a medium (book2_final, nested: the world
+    put under one bvh_node) walks its objects as the list does, so the media
+    draw from the same stream positions (the flattener still
+    refuses such a node for the GPU)."""
     flat, sf = render(host_render, tmp_path, scene, nx, ny, spp, 50, 11)
     tree, st = render(host_render, tmp_path, scene, nx, ny, spp, 50, 11, bvh=True)
     assert sf == st
