@@ -23,6 +23,32 @@
 #define M_PI 3.14159265358979323846
 #endif
 
+/* libm calls of the path.  The default build calls glibc's, as the
+ * reference does.  RTW_ORACLE_DEVLIBM (librtw_oracle_devlibm.so, the checker
+ * of the strict-radiance GPU build) calls the device's own functions instead
+ * (oracle/devlibm.cpp over raytracingweekend_amd/csrc/rtw_math.h), so that
+ * every other operation can be compared with the GPU to the last bit; the
+ * device functions' distance to glibc's is tested on its own
+ * (tests/test_sincos.py). */
+#ifdef RTW_ORACLE_DEVLIBM
+double rtw_devlibm_cos(double x);
+double rtw_devlibm_sin(double x);
+double rtw_devlibm_sin_tex(double x);
+double rtw_devlibm_log(double x);
+double rtw_devlibm_pow5(double x);
+#define O_COS(x) rtw_devlibm_cos(x)
+#define O_SIN(x) rtw_devlibm_sin(x)
+#define O_SIN_TEX(x) rtw_devlibm_sin_tex(x)
+#define O_LOG(x) rtw_devlibm_log(x)
+#define O_POW5(x) rtw_devlibm_pow5(x)
+#else
+#define O_COS(x) cos(x)
+#define O_SIN(x) sin(x)
+#define O_SIN_TEX(x) sin(x)
+#define O_LOG(x) log(x)
+#define O_POW5(x) pow((x), 5)
+#endif
+
 /* ------------------------------------------------------------------ */
 /* vec3 (vec3.h:9-91)                                                  */
 /* ------------------------------------------------------------------ */
@@ -120,8 +146,8 @@ static v3 random_cosine_direction(rng* g) {
     double r2 = random_double(g, 0.0, 1.0);
     double z = sqrt(1 - r2);
     double phi = 2 * M_PI * r1;
-    double x = cos(phi) * sqrt(r2);
-    double y = sin(phi) * sqrt(r2);
+    double x = O_COS(phi) * sqrt(r2);
+    double y = O_SIN(phi) * sqrt(r2);
     return mk(x, y, z);
 }
 
@@ -131,8 +157,8 @@ static v3 random_to_sphere(rng* g, double radius, double distance_squared) {
     double r2 = random_double(g, 0.0, 1.0);
     double z = 1 + r2 * (sqrt(1 - radius * radius / distance_squared) - 1);
     double phi = 2 * M_PI * r1;
-    double x = cos(phi) * sqrt(1 - z * z);
-    double y = sin(phi) * sqrt(1 - z * z);
+    double x = O_COS(phi) * sqrt(1 - z * z);
+    double y = O_SIN(phi) * sqrt(1 - z * z);
     return mk(x, y, z);
 }
 
@@ -308,7 +334,7 @@ static int medium_hit(const rtw_scene_desc* S, const rtw_entry* e, const ray* rw
             if (rec1.t >= rec2.t) return 0;
             if (rec1.t < 0) rec1.t = 0;
             double distance_inside_boundary = (rec2.t - rec1.t) * len(r->d);
-            double hit_distance = -(1 / e->density) * log(rnd01(g));
+            double hit_distance = -(1 / e->density) * O_LOG(rnd01(g));
             if (hit_distance < distance_inside_boundary) {
                 rec->t = rec1.t + hit_distance / len(r->d);
                 rec->p = at(r, rec->t);
@@ -409,12 +435,12 @@ static v3 texture_value(const rtw_scene_desc* S, int id, v3 p) {
     switch (t->type) {
     case RTW_TEX_CONSTANT: return lda(t->color);
     case RTW_TEX_CHECKER: { /* texture.h:38-49 */
-        double sines = sin(10.0 * p.x) * sin(10.0 * p.y) * sin(10.0 * p.z);
+        double sines = O_SIN_TEX(10.0 * p.x) * O_SIN_TEX(10.0 * p.y) * O_SIN_TEX(10.0 * p.z);
         return texture_value(S, sines < 0 ? t->odd : t->even, p);
     }
     default: { /* texture.h:57-68: vec3(1,1,1) * 0.5f * (1 + sin(scale*p.z + 10*turb(p))) */
         double pp[3] = {p.x, p.y, p.z};
-        double s = 1 + sin(t->scale * p.z + 10 * rtw_oracle_turb(S, pp));
+        double s = 1 + O_SIN_TEX(t->scale * p.z + 10 * rtw_oracle_turb(S, pp));
         double v = (1.0 * (double)0.5f) * s;
         return mk(v, v, v);
     }
@@ -504,7 +530,7 @@ static int refract(v3 v, v3 n, double ni_over_nt, v3* refracted) {
 static double schlick(double cosine, double ref_idx) {
     double r0 = (1 - ref_idx) / (1 + ref_idx);
     r0 = r0 * r0;
-    return r0 + (1 - r0) * pow((1 - cosine), 5);
+    return r0 + (1 - r0) * O_POW5(1 - cosine);
 }
 
 static v3 color(const rtw_scene_desc* S, const ray* r, int depth, rng* g, trace_ctx* tc) {

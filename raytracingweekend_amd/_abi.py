@@ -137,29 +137,37 @@ SIGNATURES = {
 _lib = None
 
 
+def load_library(path) -> C.CDLL:
+    """Load a build of the library (librtw.so, or a variant such as
+    _build/librtw_strict.so) with the C ABI's signatures.  Raises if it is
+    missing: there is no CPU fallback."""
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7
+    # (same soname as /opt/rocm's), and torch's GPU init fails if the
+    # system runtime was loaded first -- so let torch load it first.
+    if os.environ.get("RTW_NO_TORCH") != "1" and "torch" not in sys.modules:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+    path = Path(path)
+    if not path.exists():
+        raise RuntimeError(f"native library {path} is missing: build it with "
+                           f"`python -m raytracingweekend_amd.build` (there is no CPU fallback)")
+    L = C.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.rtw_abi_version() != RTW_ABI_VERSION:
+        raise RuntimeError(f"{path.name} ABI version mismatch; rebuild")
+    return L
+
+
 def lib():
     """Load librtw.so (once).  Raises if the native library is missing."""
     global _lib
     if _lib is None:
-        # One HIP runtime per process: torch bundles its own libamdhip64.so.7
-        # (same soname as /opt/rocm's), and torch's GPU init fails if the
-        # system runtime was loaded first -- so let torch load it first.
-        if os.environ.get("RTW_NO_TORCH") != "1" and "torch" not in sys.modules:
-            try:
-                import torch  # noqa: F401
-            except ImportError:
-                pass
-        if not LIB_PATH.exists():
-            raise RuntimeError(f"native library {LIB_PATH} is missing: build it with "
-                               f"`python -m raytracingweekend_amd.build` (there is no CPU fallback)")
-        L = C.CDLL(str(LIB_PATH))
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
-        if L.rtw_abi_version() != RTW_ABI_VERSION:
-            raise RuntimeError("librtw.so ABI version mismatch; rebuild")
-        _lib = L
+        _lib = load_library(LIB_PATH)
     return _lib
 
 

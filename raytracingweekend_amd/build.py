@@ -2,6 +2,8 @@
 GPU box with the repository snapshot).
 
   raytracingweekend_amd/librtw.so     HIP kernels (gfx950) + C ABI + host scene API
+  raytracingweekend_amd/_build/librtw_strict.so
+                                      the strict-radiance build (RTW_STRICT_RADIANCE)
   raytracingweekend_amd/rtw_render    C++ host program (the reference's main())
   oracle/_ref/librtw_oracle.so        test-only C restatement (oracle/Makefile)
   oracle/_ref/rtw_ref                 test-only reference harness, only where
@@ -161,8 +163,28 @@ def build_test_tools(force: bool = False) -> None:
             _run([HIPCC, *DEVICE, *COMMON, *INCLUDES, "-x", "hip", str(src), "-o", str(out)])
 
 
+STRICT_LIB = BUILD / "librtw_strict.so"
+
+
+def build_strict_library(force: bool = False) -> Path:
+    """_build/librtw_strict.so: the strict-radiance build (RTW_STRICT_RADIANCE:
+    the reference's radiance arithmetic, each path's factors folded
+    inside-out as color() returns them), checked to the last bit against the
+    oracle's device-libm build by tests/test_gpu_strict.py."""
+    # (host=True: its own host objects too, so a concurrent build_library
+    # never compiles into the same object file)
+    out = build_variant_library("strict", ["RTW_STRICT_RADIANCE=1"], force, host=True)
+    assert out == STRICT_LIB
+    return out
+
+
 def build_all(force: bool = False) -> None:
-    build_library(force)
+    # the product library and the strict-radiance build compile their
+    # kernels concurrently (one translation unit each)
+    with ThreadPoolExecutor(max_workers=2) as ex:
+        jobs = [ex.submit(build_library, force), ex.submit(build_strict_library, force)]
+        for j in jobs:
+            j.result()
     build_cli(force)
     build_oracle(force)
     build_test_tools(force)

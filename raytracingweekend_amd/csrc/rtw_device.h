@@ -36,8 +36,18 @@ constexpr double kInvPi = 1.0 / kPi;
 // positive real), the rect light's distance^2 / (cosine area) with one
 // division.  Paths, traversal counts and every decision stay the
 // reference's; the radiance moves by a few ulps (the parity bound is 1e-4).
+// RTW_STRICT_RADIANCE (a build of its own, librtw_strict.so: tests and
+// maintainers' checks): the reference's radiance arithmetic exactly -- these
+// reorderings off, and each path's factors folded inside-out at its end as
+// the recursion of color() folds them (rtw_kernels.hip, k_persist).
+#ifndef RTW_STRICT_RADIANCE
+#define RTW_STRICT_RADIANCE 0
+#endif
 #ifndef RTW_RADIANCE_FAST
-#define RTW_RADIANCE_FAST 1
+#define RTW_RADIANCE_FAST (!RTW_STRICT_RADIANCE)
+#endif
+#if RTW_STRICT_RADIANCE && RTW_RADIANCE_FAST
+#error "RTW_STRICT_RADIANCE needs RTW_RADIANCE_FAST 0"
 #endif
 // ... and (RTW_RADIANCE_RCP) the remaining radiance-only quotients -- the
 // lambertian factor, the rect light's pdf, the sphere light's 1 / solid angle -- as
@@ -2446,15 +2456,8 @@ RTW_D bool refract(d3 v, d3 n, double ni_over_nt, d3& refracted) {  // material.
     return false;
 }
 
-// x^5 in double-double (exact products through fma), rounded once: within
-// a hair of the correctly rounded x^5, i.e. at least as accurate as glibc's
-// pow(x, 5) the reference calls (< 0.52 ulp) and far cheaper than ocml pow.
-RTW_D double pow5(double x) {
-    const double x2 = x * x, e2 = fma(x, x, -x2);
-    const double x4 = x2 * x2, e4 = fma(x2, x2, -x4) + 2.0 * x2 * e2;
-    const double x5 = x4 * x, e5 = fma(x4, x, -x5) + e4 * x;
-    return x5 + e5;
-}
+// pow(x, 5) of schlick: rtw_math.h pow5 (double-double, shared with the
+// strict-radiance oracle build)
 
 // material.h:44-49 with r0 = ((1 - ref_idx) / (1 + ref_idx))^2 precomputed
 // per material on the host (same expression, same rounding)

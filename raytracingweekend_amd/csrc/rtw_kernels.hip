@@ -104,6 +104,12 @@ struct job_t {
     int32_t nx, ny, row_begin, row_step, s_begin, max_depth;
     uint32_t spp_pass;   // samples per pixel in this pass
     double* L;           // per-sample radiance, L[3q + c] (pass-local sample id q)
+#if RTW_STRICT_RADIANCE
+    // per-thread factor logs of the strict build: bounce k of the path on
+    // global thread g at flog[4 (k * flog_threads + g)] = (m.x, m.y, m.z, pdf)
+    double* flog;
+    uint32_t flog_threads;
+#endif
 };
 
 // Pass-local sample ids are sample-major: q = sample * npix + pixel, so a
@@ -360,10 +366,14 @@ enum { SEG_CONTINUE = 0, SEG_END = 1, SEG_END_ZERO = 2 };
 // continuation ray into the path's slot, radiance store), so no value of a
 // branch is live across the merge of the exec-masked branches, which run
 // one after the other.
+//   cont_mp(m, pdf, next)  (RTW_STRICT_RADIANCE, the lambertian bounce) the
+//                   path continues with the factor m / pdf, m = attenuation
+//                   * scattering_pdf, kept apart for the inside-out fold
 struct seg_out {
     d3 w;      // f or E
     ray next;  // SEG_CONTINUE only
     RTW_D void cont(const d3& f, const ray& nr) { w = f, next = nr; }
+    RTW_D void cont_mp(const d3& m, double pdf, const ray& nr) { cont(m / pdf, nr); }
     RTW_D void end(const d3& E) { w = E; }
     RTW_D void end_zero() {}
 };
@@ -373,11 +383,26 @@ struct fn_sink {  // a sink from three callables
     E e;
     Z z;
     RTW_D void cont(const d3& f, const ray& nr) { c(f, nr); }
+    RTW_D void cont_mp(const d3& m, double pdf, const ray& nr) { c(m / pdf, nr); }
     RTW_D void end(const d3& L) { e(L); }
     RTW_D void end_zero() { z(); }
 };
 template <class C, class E, class Z>
 RTW_D fn_sink<C, E, Z> make_sink(C c, E e, Z z) { return fn_sink<C, E, Z>{c, e, z}; }
+// ... and from four: cont_mp of its own (the strict build's k_persist)
+template <class C, class M, class E, class Z>
+struct fn_sink4 {
+    C c;
+    M cm;
+    E e;
+    Z z;
+    RTW_D void cont(const d3& f, const ray& nr) { c(f, nr); }
+    RTW_D void cont_mp(const d3& m, double pdf, const ray& nr) { cm(m, pdf, nr); }
+    RTW_D void end(const d3& L) { e(L); }
+    RTW_D void end_zero() { z(); }
+};
+template <class C, class M, class E, class Z>
+RTW_D fn_sink4<C, M, E, Z> make_sink4(C c, M cm, E e, Z z) { return fn_sink4<C, M, E, Z>{c, cm, e, z}; }
 
 // One segment of color() (RayTracingWeekend.cpp:52-159) for path x whose
 // world hit is (t, prim); returns the outcome (SEG_*) after handing it to
@@ -491,6 +516,19 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
         // attenuation * scattering_pdf / pdf_val as one scalar quotient
         const double w = cosine < 0 ? 0 : rad_div(cosine, kPi * pdf_val);
         return scatter(texture_value<M>(S, m.texture, p) * w, p, dir);
+#elif RTW_STRICT_RADIANCE
+        // the reference's ((attenuation * scattering_pdf) * color) / pdf_val
+        // (RayTracingWeekend.cpp:129-132): m and pdf_val go to the path's
+        // factor log; the fold applies them around the returned color
+        const double spdf = cosine < 0 ? 0 : cosine / kPi;
+        if (depth <= 1) {
+            sk.end_zero();
+            return SEG_END_ZERO;
+        }
+        sk.cont_mp(texture_value<M>(S, m.texture, p) * spdf, pdf_val, ray{p, dir, r.t});
+        x.rng = rng;
+        x.depth = depth - 1;
+        return SEG_CONTINUE;
 #else
         const double spdf = cosine < 0 ? 0 : cosine / kPi;
         return scatter((texture_value<M>(S, m.texture, p) * spdf) / pdf_val, p, dir);
@@ -993,6 +1031,32 @@ void k_persist(persist_args) {
                 o[0] = L.x, o[1] = L.y, o[2] = L.z;
             };
             ray nr;
+#if RTW_STRICT_RADIANCE
+            // the path's factors in its thread's log, folded inside-out at its
+            // end: c = E, then c = (m_k * c) / pdf_k for k = last .. 0 -- the
+            // returns of the recursive color() (RayTracingWeekend.cpp:107,
+            // 129-132; emitted of a scattering material is 0 and 0 + c == c),
+            // specular bounces logged with pdf 1 (x / 1 == x)
+            const uint32_t kb = (uint32_t)A2.J.max_depth - x.depth;  // this segment's bounce
+            const size_t gth = (size_t)blockIdx.x * kPBlock + tid;
+            double* const flog = A2.J.flog;
+            const size_t nth = A2.J.flog_threads;
+            auto log_factor = [&](const d3& m, double pdf, const ray& r) {
+                double* e = flog + 4 * ((size_t)kb * nth + gth);
+                e[0] = m.x, e[1] = m.y, e[2] = m.z, e[3] = pdf;
+                nr = r;
+            };
+            auto fold = [&](d3 c) {
+                for (int k = (int)kb - 1; k >= 0; --k) {
+                    const double* e = flog + 4 * ((size_t)k * nth + gth);
+                    c = (d3{e[0], e[1], e[2]} * c) / e[3];
+                }
+                radiance(c);
+            };
+            auto sk = make_sink4([&](const d3& f, const ray& r) { log_factor(f, 1.0, r); },
+                                 [&](const d3& m, double pdf, const ray& r) { log_factor(m, pdf, r); },
+                                 [&](const d3& E) { fold(E); }, [&]() { fold(d3{0.0, 0.0, 0.0}); });
+#else
             auto sk = make_sink(
                 [&](const d3& f, const ray& r) {
                     s_thr[0][me] *= f.x, s_thr[1][me] *= f.y, s_thr[2][me] *= f.z;
@@ -1008,6 +1072,7 @@ void k_persist(persist_args) {
                     const double z = in_place<0>();
                     radiance(d3{z, z, z});
                 });
+#endif
             const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0,
                                        (F & F_NOLIGHTS) != 0>(SS, x, h.t, h.prim, sk, pf);
             if (out != SEG_CONTINUE)
@@ -1952,6 +2017,7 @@ struct handle_t {
     dev_buf hits;
     dev_buf radiance; // per-sample planes of one pass
     dev_buf run;      // per-pixel running sums
+    dev_buf flog;     // RTW_STRICT_RADIANCE: per-thread factor logs (job_t::flog)
     dev_buf accum;    // device accum when the caller passes a host pointer
     dev_buf ctrs;
     dev_buf camera;                // device copy of the call's camera
@@ -2906,7 +2972,8 @@ void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t s
     g_node_packet = 0;
     static const bool sorted = [] {
         bool v;
-        return sort_forced(v) ? v : (FF & (F_WBVH | F_GBVH)) == 0;
+        // (the strict build folds each path's factors in k_persist)
+        return !RTW_STRICT_RADIANCE && (sort_forced(v) ? v : (FF & (F_WBVH | F_GBVH)) == 0);
     }();
     if (sorted) {
         if (name) *name = kname("k_persist_sort", FF, MM, LL);
@@ -3352,6 +3419,7 @@ extern "C" void rtw_scene_free(void* handle) {
     h->hits.release();
     h->radiance.release();
     h->run.release();
+    h->flog.release();
     h->accum.release();
     h->ctrs.release();
     h->camera.release();
@@ -3447,6 +3515,13 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     J.nx = R.nx, J.ny = R.ny, J.row_begin = R.row_begin, J.row_step = row_step;
     J.max_depth = R.max_depth;
     J.L = static_cast<double*>(h->radiance.p);
+#if RTW_STRICT_RADIANCE
+    // a factor log per thread of the largest resident grid (2 048 threads per
+    // CU), one 32-B entry per bounce
+    J.flog_threads = (uint32_t)h->cus * 2048u;
+    if ((rc = h->flog.ensure((size_t)J.flog_threads * (size_t)R.max_depth * 32))) return rc;
+    J.flog = static_cast<double*>(h->flog.p);
+#endif
 
     const int grid = h->grid;
     const int regen_grid = (int)((pool + kRegenSlots - 1) / kRegenSlots);
@@ -3495,6 +3570,9 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                                                         h->S.render_type != RTW_RENDER_NORMAL,
                                                     pin));
 
+    if (RTW_STRICT_RADIANCE && !persistent)
+        return rtw_fail(RTW_ERR_UNSUPPORTED, "the strict-radiance build renders with the persistent kernel only "
+                                             "(RTW_MODE=wavefront or a scene without a persistent instantiation)");
     for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
         J.total = (uint32_t)(S_pass * npix);

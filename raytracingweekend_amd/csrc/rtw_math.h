@@ -61,6 +61,17 @@ RTW_HD void sincos_azimuth(double x, double& sn, double& cs) {
 // (33 significant bits each) are still exact and the remainder carries 119
 // bits of pi/2.  Within an ulp of glibc's sin over that range
 // (tests/cpp/sincos_check.cpp); callers take their own path outside it.
+// x^5 in double-double (exact products through fma), rounded once: within
+// a hair of the correctly rounded x^5, i.e. at least as accurate as glibc's
+// pow(x, 5) the reference calls (material.h:44-49, < 0.52 ulp) and far
+// cheaper than ocml pow.
+RTW_HD double pow5(double x) {
+    const double x2 = x * x, e2 = __builtin_fma(x, x, -x2);
+    const double x4 = x2 * x2, e4 = __builtin_fma(x2, x2, -x4) + 2.0 * x2 * e2;
+    const double x5 = x4 * x, e5 = __builtin_fma(x4, x, -x5) + e4 * x;
+    return x5 + e5;
+}
+
 RTW_HD bool sin_wide_ok(double x) { return __builtin_fabs(x) <= 0x1p19; }
 RTW_HD double sin_wide(double x) {
     double s, c;
