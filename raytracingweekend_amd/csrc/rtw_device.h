@@ -188,7 +188,11 @@ RTW_D double canon_raw(uint32_t r1, uint32_t r2) {
     const double e2 = (double)(r2 - 1u);
     double sum = 0.0 + e1 * 1.0;
     sum = sum + e2 * kCanonR;
-    double r = div_rcp(sum, kCanonDiv, kCanonRcp);  // sum in [0, 2^62]: always in the guard
+#ifndef RTW_CANON_ONESTEP
+#define RTW_CANON_ONESTEP 1
+#endif
+    // sum in [0, 2^62]: one Markstein step (rtw_div.h div_canon); 0: div_rcp's two
+    double r = RTW_CANON_ONESTEP ? div_canon(sum) : div_rcp(sum, kCanonDiv, kCanonRcp);
     return r >= 1.0 ? kOneMinusUlp : r;
 }
 RTW_D double canon(uint32_t& s) {

@@ -39,6 +39,22 @@ RTW_HD double div_rcp(double a, double b, double y) {
     return a == 0.0 ? q0 : __builtin_fma(r1, y, q1);  // q0 carries 0's sign rule
 }
 
+// generate_canonical's sum / (R * R), R * R rounded to b = 2^62 - 2^33 (the
+// divisor libstdc++ forms, kCanonDiv), for 0 <= sum <= 2^62: ONE correction
+// step.  y = RN(1/b) = 2^-62 (1 + 2^-29) lies within 2^-57.9 (relative) of
+// 1/b = 2^-62 (1 + 2^-29 + 2^-58 + ...), so q0 = RN(sum * y) is within
+// 0.534 ulp of sum / b -- faithful -- and Markstein's theorem (y = RN(1/b),
+// q0 within 1 ulp, r = fma(-b, q0, sum) exact) makes fma(r, y, q0) the
+// correctly rounded quotient; sum = +0 gives +0.  div_rcp's second step and
+// its zero select are not needed (tests/cpp/div_check.cpp: every canonical
+// sum form, bit for bit against IEEE division).
+RTW_HD double div_canon(double sum) {
+    constexpr double b = 4611686009837453312.0;  // 2^62 - 2^33
+    constexpr double y = 0x1.00000008p-62;       // RN(1 / b) = 2^-62 (1 + 2^-29)
+    const double q0 = sum * y;
+    return __builtin_fma(__builtin_fma(-b, q0, sum), y, q0);
+}
+
 // Quotient, reciprocal and remainders stay normal: |b| in [2^-500, 2^500],
 // a = 0 or |a| in [2^-500, 2^500].  (NaN / inf operands fail the test.)
 RTW_HD bool div_rcp_ok_b(double b) {

@@ -1141,16 +1141,49 @@ enum { K_LAMB = 0, K_DIEL, K_METAL, K_ISO, K_EMIT, K_MISS, K_IDLE, K_N };
 #endif
 constexpr int kSortBlock = RTW_SORT_BLOCK;  // paths regrouped together (one workgroup)
 constexpr int kSortWaves = kSortBlock / 64;
+// HOME_RAY (RTW_SORT_HOME_RAY): a path's ray and sample id live in its home
+// slot beside its throughput, so the exchange moves only the record's home
+// index, hit (t, prim), engine and depth -- 5 values instead of 12 -- and the
+// lanes read the ray from the home slot where they trace or shade it.
+#ifndef RTW_SORT_HOME_RAY
+#define RTW_SORT_HOME_RAY 0
+#endif
 template <int F, int M, bool LDS>
 __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist_sort(persist_args) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_kc[kSortWaves][K_N];  // per wave, lanes per key
     __shared__ uint32_t s_seg[kSortWaves];
-    // the exchange: one path per slot (SoA)
-    __shared__ double x_o[3][kSortBlock], x_d[3][kSortBlock], x_tm[kSortBlock], x_t[kSortBlock];
+    constexpr bool HR = RTW_SORT_HOME_RAY != 0;
+    constexpr int kX = HR ? 1 : kSortBlock;  // exchange arrays HOME_RAY does without
+    // the exchange: one path per slot (SoA); HOME_RAY: the ray and sample id
+    // at the record's home instead (h_o, h_d, h_tm, h_q)
+    __shared__ double x_o[3][kX], x_d[3][kX], x_tm[kX], x_t[kSortBlock];
     __shared__ int32_t x_prim[kSortBlock];
-    __shared__ uint32_t x_rng[kSortBlock], x_depth[kSortBlock], x_q[kSortBlock], x_home[kSortBlock];
+    __shared__ uint32_t x_rng[kSortBlock], x_depth[kSortBlock], x_q[kX], x_home[kSortBlock];
+    constexpr int kH = HR ? kSortBlock : 1;
+    __shared__ double h_o[3][kH], h_d[3][kH], h_tm[(F & F_STATIC) ? 1 : kH];
+    __shared__ uint32_t h_q[kH];
+    // the record's ray / sample id in slot `s` (exchange slot, or home)
+    auto ray_at = [&](uint32_t s) {
+        if constexpr (HR)
+            return ray{d3{h_o[0][s], h_o[1][s], h_o[2][s]}, d3{h_d[0][s], h_d[1][s], h_d[2][s]},
+                       (F & F_STATIC) ? 0.0 : h_tm[s]};
+        else
+            return ray{d3{x_o[0][s], x_o[1][s], x_o[2][s]}, d3{x_d[0][s], x_d[1][s], x_d[2][s]},
+                       (F & F_STATIC) ? 0.0 : x_tm[s]};
+    };
+    auto put_ray = [&](uint32_t s, const ray& r) {
+        if constexpr (HR) {
+            h_o[0][s] = r.o.x, h_o[1][s] = r.o.y, h_o[2][s] = r.o.z;
+            h_d[0][s] = r.d.x, h_d[1][s] = r.d.y, h_d[2][s] = r.d.z;
+            if constexpr (!(F & F_STATIC)) h_tm[s] = r.t;
+        } else {
+            x_o[0][s] = r.o.x, x_o[1][s] = r.o.y, x_o[2][s] = r.o.z;
+            x_d[0][s] = r.d.x, x_d[1][s] = r.d.y, x_d[2][s] = r.d.z;
+            if constexpr (!(F & F_STATIC)) x_tm[s] = r.t;
+        }
+    };
     // Path throughputs stay put: each path record (live or idle) owns one
     // home slot of s_thr and carries its index through the exchange, so the
     // throughput is read and written only where shading uses it and is never
@@ -1214,12 +1247,13 @@ void k_persist_sort(persist_args) {
                 if (got) {
                     const ray r = camera_sample(J, q, x.rng);
                     const uint32_t me = threadIdx.x;
-                    x_o[0][me] = r.o.x, x_o[1][me] = r.o.y, x_o[2][me] = r.o.z;
-                    x_d[0][me] = r.d.x, x_d[1][me] = r.d.y, x_d[2][me] = r.d.z;
-                    if (!(F & F_STATIC)) x_tm[me] = r.t;  // F_STATIC: never read
-                    x_q[me] = q;
+                    const uint32_t home = x_home[me];
+                    put_ray(HR ? home : me, r);  // (F_STATIC: the time is never read)
+                    if constexpr (HR)
+                        h_q[home] = q;
+                    else
+                        x_q[me] = q;
                     x.depth = (uint32_t)J.max_depth;
-                    const uint32_t home = x_home[threadIdx.x];
                     s_thr[0][home] = 1.0, s_thr[1][home] = 1.0, s_thr[2][home] = 1.0;
                 }
             }
@@ -1231,8 +1265,7 @@ void k_persist_sort(persist_args) {
         int key = K_IDLE;
         if (x.depth != 0) {
             const uint32_t me = threadIdx.x;
-            x.r = ray{d3{x_o[0][me], x_o[1][me], x_o[2][me]}, d3{x_d[0][me], x_d[1][me], x_d[2][me]},
-                      (F & F_STATIC) ? 0.0 : x_tm[me]};
+            x.r = ray_at(HR ? x_home[me] : me);
             const persist_args& A = args_now();
             const scene SS = LDS ? lds_scene(A.S, A.base, s_scene) : A.S;
             const hit_state h = world_closest<F>(A.S, x.r, x.rng);
@@ -1255,7 +1288,7 @@ void k_persist_sort(persist_args) {
         // 3. counting sort of the block's paths by key (the record's home and
         // sample id are read from the lane's own slot before the barrier that
         // precedes the exchange's writes)
-        const uint32_t my_home = x_home[threadIdx.x], my_q = x_q[threadIdx.x];
+        const uint32_t my_home = x_home[threadIdx.x], my_q = HR ? 0u : x_q[threadIdx.x < kX ? threadIdx.x : 0];
         uint32_t rank_in_wave = 0;
         // keys the scene's material set cannot produce are skipped (their
         // counts stay 0; keep s_kc's slots zero for the prefix below)
@@ -1289,17 +1322,13 @@ void k_persist_sort(persist_args) {
         pk.mark(PS_HIT);
         // 4. move every path to the slot of its rank (an idle record's ray
         // is garbage and stays behind)
-        if (x.depth != 0) {
-            x_o[0][dst] = x.r.o.x, x_o[1][dst] = x.r.o.y, x_o[2][dst] = x.r.o.z;
-            x_d[0][dst] = x.r.d.x, x_d[1][dst] = x.r.d.y, x_d[2][dst] = x.r.d.z;
-            if (!(F & F_STATIC)) x_tm[dst] = x.r.t;
-        }
+        if (!HR && x.depth != 0) put_ray(dst, x.r);
         x_home[dst] = my_home;
         x_t[dst] = th;
         x_prim[dst] = hp;
         x_rng[dst] = x.rng;
         x_depth[dst] = x.depth;
-        x_q[dst] = my_q;
+        if constexpr (!HR) x_q[dst] = my_q;
         __syncthreads();
         // (opaque, so the exchange's per-lane LDS addresses are formed here
         // from one register, not hoisted out of the loop one per array)
@@ -1310,24 +1339,21 @@ void k_persist_sort(persist_args) {
         pk.mark(PS_SAMPLE);
         // 5. shading, now mostly one branch per wave
         if (x.depth != 0) {
-            x.r = ray{d3{x_o[0][me], x_o[1][me], x_o[2][me]}, d3{x_d[0][me], x_d[1][me], x_d[2][me]},
-                      (F & F_STATIC) ? 0.0 : x_tm[me]};
+            x.r = ray_at(HR ? x_home[me] : me);
             const persist_args& A = args_now();
             const scene SS = LDS ? lds_scene(A.S, A.base, s_scene) : A.S;
             prof_t pf;
             // the outcome is applied inside the branch that produced it
             auto radiance = [&](const d3& L) {
-                double* o = A.J.L + 3 * (size_t)x_q[me];
+                double* o = A.J.L + 3 * (size_t)(HR ? h_q[x_home[me]] : x_q[me]);
                 o[0] = L.x, o[1] = L.y, o[2] = L.z;
             };
             auto sk = make_sink(
                 [&](const d3& f, const ray& nr) {
                     const uint32_t home = x_home[me];
                     s_thr[0][home] *= f.x, s_thr[1][home] *= f.y, s_thr[2][home] *= f.z;
-                    // the continuation ray waits in the lane's own slot
-                    x_o[0][me] = nr.o.x, x_o[1][me] = nr.o.y, x_o[2][me] = nr.o.z;
-                    x_d[0][me] = nr.d.x, x_d[1][me] = nr.d.y, x_d[2][me] = nr.d.z;
-                    if (!(F & F_STATIC)) x_tm[me] = nr.t;
+                    // the continuation ray waits in the lane's own slot (HOME_RAY: the home's)
+                    put_ray(HR ? home : me, nr);
                 },
                 [&](const d3& E) {
                     const uint32_t home = x_home[me];

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 
 #include "rtw_div.h"
 
@@ -44,8 +45,38 @@ static void check(double a, double b) {
     }
 }
 
+// div_canon: generate_canonical's sum = (e1 + e2 * R) for raw draws e1, e2 in
+// [0, 2^31 - 3] (R = 2^31 - 2, libstdc++'s two-draw form, rtw_device.h
+// canon_raw) divided by kCanonDiv
+static long long ccases = 0, cbad = 0;
+static void check_canon(uint64_t e1, uint64_t e2) {
+    const double R = 2147483646.0, b = 4611686009837453312.0;
+    double sum = 0.0 + (double)e1 * 1.0;
+    sum = sum + (double)e2 * R;
+    const double q = rtwd::div_canon(sum), want = sum / b;
+    ++ccases;
+    if (bits(q) != bits(want) && ++cbad <= 10) std::printf("canon mismatch sum=%a got=%a want=%a\n", sum, q, want);
+}
+
 int main(int argc, char** argv) {
     const long long n = argc > 1 ? std::atoll(argv[1]) : 1000000;
+    {
+        if (rtwd::div_canon(0.0) != 0.0 || std::signbit(rtwd::div_canon(0.0))) ++cbad;
+        const uint64_t top = 2147483645ull;  // 2^31 - 3
+        for (uint64_t e2 : {(uint64_t)0, (uint64_t)1, (uint64_t)2, top - 1, top})
+            for (uint64_t e1 = 0; e1 < 200000; ++e1) check_canon(e1, e2), check_canon(top - e1, e2);
+        for (long long k = 0; k < 20 * n; ++k) check_canon(next() % (top + 1), next() % (top + 1));
+        // sums next to every power of two (binade edges, where q0's error bound is widest)
+        for (int e = 31; e <= 62; ++e)
+            for (int d = -3000; d <= 3000; ++d) {
+                const double s = std::ldexp(1.0, e) + d * std::ldexp(1.0, e - 52 > 0 ? e - 52 : 0);
+                const double want = s / 4611686009837453312.0;
+                ++ccases;
+                if (bits(rtwd::div_canon(s)) != bits(want) && ++cbad <= 10)
+                    std::printf("canon mismatch edge sum=%a\n", s);
+            }
+        std::printf("canon cases %lld mismatches %lld\n", ccases, cbad);
+    }
     const double consts[] = {3.14159265358979323846, 4611686009837453312.0, 2147483646.0, 6.283185307179586,
                              0.1, 3.0, 555.0};
     for (long long k = 0; k < n; ++k) {
@@ -83,5 +114,5 @@ int main(int argc, char** argv) {
     for (double a : edge)
         for (double b : edge) check(a, b);
     std::printf("cases %lld mismatches %lld\n", cases, bad);
-    return bad ? 1 : 0;
+    return (bad || cbad) ? 1 : 0;
 }

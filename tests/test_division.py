@@ -15,4 +15,5 @@ def test_markstein_division_is_ieee(tmp_path):
                     "-o", str(exe)], check=True)
     r = subprocess.run([str(exe), "2000000"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "mismatches 0" in r.stdout
+    assert "canon cases" in r.stdout and "canon cases 0" not in r.stdout
+    assert r.stdout.count("mismatches 0") == 2, r.stdout
