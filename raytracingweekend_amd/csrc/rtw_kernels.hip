@@ -2117,9 +2117,11 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         // again later in the walk (the reference's second list walk) reuses
         // the boundary distances its first visit found on the same ray; the
         // first kMediumSlots media visited twice get a slot
+        // (RTW_MEDIUM_CACHE builds only: the default walk reads no slot, so
+        // its visits carry the bare entry index)
         std::map<int, int> slot_of, seen;
         for (int32_t e : media)
-            if (d->entries[e].kind == RTW_ENTRY_MEDIUM) ++seen[e];
+            if (RTW_MEDIUM_CACHE && d->entries[e].kind == RTW_ENTRY_MEDIUM) ++seen[e];
         for (int32_t& v : media) {
             const int e = v;
             if (d->entries[e].kind != RTW_ENTRY_MEDIUM || seen[e] < 2) continue;
