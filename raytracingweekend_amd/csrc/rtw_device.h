@@ -159,11 +159,35 @@ __device__ __forceinline__ double rad_div(double a, double b) {
 }
 RTW_HD double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RTW_HD double len2(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+// RTW_SQRT_CORE: fp64 square roots as rtw_div.h's sqrt_w (the compiler's own
+// sequence without its range scaling and class fixup, taken when the whole
+// wave is in range; bit for bit the same value) or sqrt_core where the range
+// is known (1 - a canonical draw).  0: the compiler's sqrt everywhere (A/B).
+#ifndef RTW_SQRT_CORE
+#define RTW_SQRT_CORE 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && RTW_SQRT_CORE
+#define RTW_SQRT(x) sqrt_w(x)
+#define RTW_SQRT_POS(x) sqrt_core(x)  // x in [2^-766, 2^1024): callers argue it
+#else
+#define RTW_SQRT(x) __builtin_sqrt(x)
+#define RTW_SQRT_POS(x) __builtin_sqrt(x)
+#endif
 RTW_HD double len(d3 a) { return __builtin_sqrt(len2(a)); }
 RTW_HD d3 cross(d3 a, d3 b) {  // vec3.h:54-59
     return d3{a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x};
 }
+#ifndef RTW_SQRT_NORM
+#define RTW_SQRT_NORM 1
+#endif
+#if RTW_SQRT_NORM
+RTW_HD d3 normalize(d3 v) { return v / RTW_SQRT(len2(v)); }  // vec3.h:61-67
+#else
 RTW_HD d3 normalize(d3 v) { return v / len(v); }  // vec3.h:61-67
+#endif
+// (the compiler's sqrt: in onb_from_w a wave-uniform branch inside the
+// frame's normalizations turned the onb into a scratch object)
+RTW_HD d3 normalize_b(d3 v) { return v / len(v); }
 RTW_HD d3 ld3(const double* p) { return d3{p[0], p[1], p[2]}; }
 
 struct ray {
@@ -271,9 +295,9 @@ RTW_D d3 random_in_unit_sphere(uint32_t& s) {
 RTW_D d3 random_cosine_direction(uint32_t& s) {  // utility.h:54-67
     const double r1 = rnd01(s);
     const double r2 = rnd01(s);
-    const double z = __builtin_sqrt(1 - r2);
+    const double z = RTW_SQRT_POS(1 - r2);  // r2 <= 1 - 2^-53: 1 - r2 >= 2^-53
     const double phi = kTwoPi * r1;
-    const double sq = __builtin_sqrt(r2);
+    const double sq = RTW_SQRT(r2);
     double sp, cp;
     sincos_azimuth(phi, sp, cp);
     return d3{cp * sq, sp * sq, z};
@@ -285,9 +309,9 @@ struct onb {
 };
 RTW_HD onb onb_from_w(d3 n) {  // onb.h:32-38
     onb b;
-    b.w = normalize(n);
+    b.w = normalize_b(n);
     const d3 a = (fabs(b.w.x) > 0.9) ? d3{0, 1, 0} : d3{1, 0, 0};
-    b.v = normalize(cross(b.w, a));
+    b.v = normalize_b(cross(b.w, a));
     b.u = cross(b.w, b.v);
     return b;
 }
@@ -518,7 +542,7 @@ RTW_D bool sphere_t(const rtw_prim& s, const ray& r, double t_min, double t_max,
     const double c = dot(oc, oc) - s.p[9];  // radius * radius
     const double disc = b * b - a * c;
     if (disc > 0) {
-        const double sq = __builtin_sqrt(disc);
+        const double sq = RTW_SQRT(disc);
         double temp = (-b - sq) / a;
         if (temp < t_max && temp > t_min) {
             t_out = temp;
@@ -783,7 +807,7 @@ RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_m
             const double c = dot(oc, oc) - q.p[9];
             const double disc = b * b - a * c;
             if (disc > 0) {
-                const double sq = __builtin_sqrt(disc);
+                const double sq = RTW_SQRT(disc);
                 double temp = (-b - sq) / a;
                 bool ok = temp < h.t && temp > t_min;
                 if (!ok) {
@@ -901,7 +925,7 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
         const double c = dot(oc, oc) - ld(p + 9);
         const double disc = b * b - a * c;
         if (disc > 0) {
-            const double sq = __builtin_sqrt(disc);
+            const double sq = RTW_SQRT(disc);
             double temp = walk_quot(-b - sq, a, ya, oka);
             bool ok = temp < h.t && temp > t_min;
             if (!ok) {
@@ -1049,7 +1073,7 @@ RTW_D void arbitrate_u(const scene& S, int pi, const ray& r, double t_min, hit_s
         const double c = dot(oc, oc) - q.p[9];
         const double disc = b * b - a * c;
         if (!(disc > 0)) return;
-        const double sq = __builtin_sqrt(disc);
+        const double sq = RTW_SQRT(disc);
         t = walk_quot(-b - sq, a, ya, oka);
         if (!(t < kDblMax && t > t_min)) {
             t = walk_quot(-b + sq, a, ya, oka);
@@ -1220,7 +1244,7 @@ RTW_D void arbitrate_a(const scene& S, int pi, const ray& r, double t_min, hit_s
         const double c = dot(oc, oc) - q.p[9];
         const double disc = b * b - a * c;
         if (!(disc > 0)) return;
-        const double sq = __builtin_sqrt(disc);
+        const double sq = RTW_SQRT(disc);
         t = walk_quot(-b - sq, a, ya, oka);
         if (!(t < kDblMax && t > t_min)) {
             t = walk_quot(-b + sq, a, ya, oka);
@@ -1938,7 +1962,7 @@ RTW_D bool medium_bounds(const scene& S, const entry_v& e, const ray& r, int n_o
         const double c = dot(oc, oc) - q.p[9];
         const double disc = b * b - a * c;
         if (!(disc > 0)) return false;
-        const double sq = __builtin_sqrt(disc);
+        const double sq = RTW_SQRT(disc);
         const double r0 = (-b - sq) / a, r1 = (-b + sq) / a;
         if (r0 < kDblMax && r0 > -kDblMax)
             t1 = r0;
@@ -2363,10 +2387,10 @@ RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
         // (magnitude only: the pdf's sign is that of the hit above; r^2 / d^2
         // stays a division, so 1 - r^2 / d^2 rounds as the reference's does
         // next to the sphere, where it cancels)
-        const double cos_theta_max = __builtin_sqrt(1 - q.p[9] / len2(ld3(q.p) - o));
+        const double cos_theta_max = RTW_SQRT(1 - q.p[9] / len2(ld3(q.p) - o));
         return rad_div(1.0, kTwoPi * (1.0 - cos_theta_max));
 #else
-        const double cos_theta_max = __builtin_sqrt(1 - q.p[9] / len2(ld3(q.p) - o));  // p[9] = radius * radius
+        const double cos_theta_max = RTW_SQRT(1 - q.p[9] / len2(ld3(q.p) - o));  // p[9] = radius * radius
         const double solid_angle = kTwoPi * (1.0 - cos_theta_max);
         return 1.0 / solid_angle;
 #endif
@@ -2429,9 +2453,9 @@ RTW_D d3 mixture_generate(const scene& S, const surf_frame& sf, d3 o, uint32_t& 
         bf.rect = false;
         a1 = 1 - q.p[9] / distance_squared;  // radius * radius / distance_squared
     }
-    const double s1 = __builtin_sqrt(a1);
+    const double s1 = RTW_SQRT(a1);
     const double z = sph ? 1 + r2 * (s1 - 1) : s1;
-    const double sq = __builtin_sqrt(sph ? 1 - z * z : r2);
+    const double sq = RTW_SQRT(sph ? 1 - z * z : r2);
     const double phi = kTwoPi * r1;
     double sp, cp;
     sincos_azimuth(phi, sp, cp);
@@ -2454,7 +2478,7 @@ RTW_D bool refract(d3 v, d3 n, double ni_over_nt, d3& refracted) {  // material.
     const double dt = dot(uv, n);
     const double disc = 1.0 - ni_over_nt * ni_over_nt * (1 - dt * dt);
     if (disc > 0) {
-        refracted = (uv - n * dt) * ni_over_nt - n * __builtin_sqrt(disc);
+        refracted = (uv - n * dt) * ni_over_nt - n * RTW_SQRT(disc);
         return true;
     }
     return false;

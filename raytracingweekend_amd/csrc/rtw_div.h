@@ -106,6 +106,37 @@ __device__ __forceinline__ uint32_t exp_bits(double v) {
 }
 __device__ __forceinline__ bool div_hw_ok_b_exp(double b) { return exp_bits(b) - 823u < 400u; }
 __device__ __forceinline__ bool div_hw_ok_a0_exp(double a) { return a == 0.0 || exp_bits(a) - 223u < 900u; }
+
+// fp64 square root without the compiler's range handling.  hipcc expands
+// sqrt(x) on gfx950 as: s = x < 2^-767 ? 256 : 0; x' = ldexp(x, s); y =
+// rsq(x'); the Goldschmidt / Newton refinement below; ldexp(g, -s/2); and a
+// class fixup returning x' for +-0 and +inf.  For positive finite x >= 2^-766
+// the scale and fixup are identities, leaving exactly this sequence, so the
+// result is bit for bit the compiler's sqrt (tests/cpp/sqrt_check.hip on the
+// card) for 7 fewer instructions (two of them fp64 ldexp).
+__device__ __forceinline__ double sqrt_core(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
+// x positive, finite, >= 2^-766 (the sign and biased exponent in the high word)
+__device__ __forceinline__ bool sqrt_core_ok(double x) {
+    const uint32_t hi = (uint32_t)(__builtin_bit_cast(unsigned long long, x) >> 32);
+    return (hi >> 20) - 257u < 1790u;
+}
+// sqrt for a wave: the core sequence when every active lane is in its range
+// (wave-uniform branch), else the compiler's sqrt -- the same value either way
+__device__ __forceinline__ double sqrt_w(double x) {
+    if (__builtin_amdgcn_ballot_w64(!sqrt_core_ok(x)) == 0) return sqrt_core(x);
+    return __builtin_sqrt(x);
+}
 #endif
 
 }  // namespace rtwd

@@ -462,7 +462,7 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
             outward = -n;
             ni_over_nt = ri;
             cosine = dot(r.d, n) / len(r.d);
-            cosine = __builtin_sqrt(1 - ri * ri * (1 - cosine * cosine));
+            cosine = RTW_SQRT(1 - ri * ri * (1 - cosine * cosine));
         } else {
             outward = n;
             ni_over_nt = S.mat_aux[2 * mat];  // 1.0 / ri, host-computed

@@ -24,6 +24,8 @@ VARIANTS = {
     "strict_radiance": T + ["-DRTW_STRICT_RADIANCE=1"],
     "strict_radiance_media": C5 + ["-DRTW_STRICT_RADIANCE=1"],
     "canon_two_steps": T + ["-DRTW_CANON_ONESTEP=0"],
+    "compiler_sqrt": T + ["-DRTW_SQRT_CORE=0"],
+    "sqrt_core_no_normalize": C5 + ["-DRTW_SQRT_NORM=0"],
     "sort_home_ray": T + ["-DRTW_SORT_HOME_RAY=1"],
     "div3_shared": T + ["-DRTW_DIV3_SHARED=1"],
     "pixel_major": T + ["-DRTW_PIXEL_MAJOR=1"],
