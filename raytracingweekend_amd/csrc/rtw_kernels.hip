@@ -127,6 +127,24 @@ struct job_t {
 #define RTW_PIXEL_MAJOR 0
 #endif
 
+// A sample's radiance record.  RTW_NT_RECORDS: non-temporal stores -- the
+// records are read back only by k_reduce after the launch, so they stream
+// past the L2 instead of evicting the lines the traversal reuses (scene,
+// nodes beyond the LDS packet, spill slots).
+#ifndef RTW_NT_RECORDS
+#define RTW_NT_RECORDS 0
+#endif
+template <typename T>
+__device__ __forceinline__ void store_record(T* o, T x, T y, T z) {
+#if RTW_NT_RECORDS
+    __builtin_nontemporal_store(x, o);
+    __builtin_nontemporal_store(y, o + 1);
+    __builtin_nontemporal_store(z, o + 2);
+#else
+    o[0] = x, o[1] = y, o[2] = z;
+#endif
+}
+
 // pass-local sample id -> pixel (i, j) and global sample index s
 __device__ __forceinline__ void sample_coords(const job_t& J, uint32_t q, int& i, int& j, int& s) {
 #if RTW_PIXEL_MAJOR
@@ -618,7 +636,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(scene S, job_t J, paths_t P, f
         prof_t pf;
         if (shade_one<M>(SS, J, P, FR, i, x, rng, ht[i], hid[i], L, q, pf)) {
             double* o = J.L + 3 * (size_t)q;
-            o[0] = L.x, o[1] = L.y, o[2] = L.z;
+            store_record(o, L.x, L.y, L.z);
             P.depth[i] = 0;
         }
     }
@@ -661,7 +679,7 @@ __global__ __launch_bounds__(kBlock) RTW_SEG_ATTR void k_segment(scene S, job_t 
         uint32_t q;
         if (shade_one<M>(SS, J, P, FR, i, x, rng, h.t, h.prim, L, q, pf)) {
             double* o = J.L + 3 * (size_t)q;
-            o[0] = L.x, o[1] = L.y, o[2] = L.z;
+            store_record(o, L.x, L.y, L.z);
             P.depth[i] = 0;
         }
         pf.mark(PS_STORE);
@@ -1028,7 +1046,7 @@ void k_persist(persist_args) {
             }
             auto radiance = [&](const d3& L) {
                 double* o = A2.J.L + 3 * (size_t)s_q[me];
-                o[0] = L.x, o[1] = L.y, o[2] = L.z;
+                store_record(o, L.x, L.y, L.z);
             };
             ray nr;
 #if RTW_STRICT_RADIANCE
@@ -1346,7 +1364,7 @@ void k_persist_sort(persist_args) {
             // the outcome is applied inside the branch that produced it
             auto radiance = [&](const d3& L) {
                 double* o = A.J.L + 3 * (size_t)(HR ? h_q[x_home[me]] : x_q[me]);
-                o[0] = L.x, o[1] = L.y, o[2] = L.z;
+                store_record(o, L.x, L.y, L.z);
             };
             auto sk = make_sink(
                 [&](const d3& f, const ray& nr) {
@@ -1395,7 +1413,7 @@ __device__ __forceinline__ void store_record_f32(double* L, uint32_t q, float x,
     o[0] = (double)x, o[1] = (double)y, o[2] = (double)z;
 #else
     float* o = reinterpret_cast<float*>(L) + 3 * (size_t)q;
-    o[0] = x, o[1] = y, o[2] = z;
+    store_record(o, x, y, z);
 #endif
 }
 

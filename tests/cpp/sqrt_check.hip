@@ -39,12 +39,18 @@ __global__ void k_check(int cls, unsigned long long n, unsigned long long* bad) 
             x = from_bits(((257ull + (r >> 52) % 1790ull) << 52) | (r & 0xFFFFFFFFFFFFFull));
         } else if (cls == 1) {  // the kernels' values: [0, 4) (1 - r2, r2, discriminants, lengths^2)
             x = (double)(r >> 11) * 0x1p-51;
-        } else if (cls == 2) {  // around the range's low edge and 1
-            const unsigned long long e = (r >> 60) & 1 ? 250ull + (r >> 52) % 16ull : 1018ull + (r >> 52) % 10ull;
+        } else if (cls == 2) {  // the range's low edge (2^-766 ...) and around 1
+            const unsigned long long e = (r >> 60) & 1 ? 257ull + (r >> 52) % 16ull : 1018ull + (r >> 52) % 10ull;
             x = from_bits((e << 52) | (r & 0xFFFFFFFFFFFFFull));
-        } else {  // anything at all (sqrt_w only): all bit patterns, with zeros and infinities mixed in
+        } else {  // anything at all (sqrt_w only): all bit patterns, with zeros, infinities and the
+                  // doubles just below the core's range (2^-774 .. 2^-766) mixed in
             const unsigned long long k = r & 15;
-            x = k == 0 ? 0.0 : k == 1 ? -0.0 : k == 2 ? __builtin_inf() : k == 3 ? -1.0 : from_bits(r);
+            x = k == 0   ? 0.0
+                : k == 1 ? -0.0
+                : k == 2 ? __builtin_inf()
+                : k == 3 ? -1.0
+                : k == 4 ? from_bits(((249ull + (r >> 52) % 8ull) << 52) | (r & 0xFFFFFFFFFFFFFull))
+                         : from_bits(r);
         }
         const double want = __builtin_sqrt(x);
         const double w = rtwd::sqrt_w(x);

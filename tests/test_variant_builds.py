@@ -25,6 +25,8 @@ VARIANTS = {
     "strict_radiance_media": C5 + ["-DRTW_STRICT_RADIANCE=1"],
     "canon_two_steps": T + ["-DRTW_CANON_ONESTEP=0"],
     "compiler_sqrt": T + ["-DRTW_SQRT_CORE=0"],
+    "nt_records": T + ["-DRTW_NT_RECORDS=1"],
+    "nt_records_fast": FAST5 + ["-DRTW_NT_RECORDS=1"],
     "sqrt_core_no_normalize": C5 + ["-DRTW_SQRT_NORM=0"],
     "sort_home_ray": T + ["-DRTW_SORT_HOME_RAY=1"],
     "div3_shared": T + ["-DRTW_DIV3_SHARED=1"],
