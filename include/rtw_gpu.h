@@ -255,9 +255,10 @@ typedef struct rtw_render_params {
                               distances, comparisons, random draws) in the
                               reference's IEEE double arithmetic; the radiance-only
                               factors (lambertian weight, pdf quotients) with fewer
-                              divisions, a few ulps off (build with
-                              -DRTW_RADIANCE_FAST=0 for the reference's own
-                              expressions there too);
+                              divisions, a few ulps off (the strict build,
+                              -DRTW_STRICT_RADIANCE=1, librtw_strict.so: the
+                              reference's own expressions, folded inside-out
+                              as color() returns them);
                               RTW_PRECISION_FP32 (1) = fast mode, single precision
                               traversal and shading, statistical parity only     */
 } rtw_render_params;
