@@ -177,8 +177,12 @@ RTW_HD double len(d3 a) { return __builtin_sqrt(len2(a)); }
 RTW_HD d3 cross(d3 a, d3 b) {  // vec3.h:54-59
     return d3{a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x};
 }
+// RTW_SQRT_NORM: normalize's length through sqrt_w too.  Measured (1 MI355X,
+// A/B, profiles/r05/ab_r5b_*.log): T 4 465 vs 4 523 without it, C5 slice 663
+// vs 676, C3 3 009 vs 3 015, C2 2 240 vs 2 243 -- its wave-uniform branches
+// in every normalization cost SGPRs (12 -> 24 spilled into VGPR lanes on T).
 #ifndef RTW_SQRT_NORM
-#define RTW_SQRT_NORM 1
+#define RTW_SQRT_NORM 0
 #endif
 #if RTW_SQRT_NORM
 RTW_HD d3 normalize(d3 v) { return v / RTW_SQRT(len2(v)); }  // vec3.h:61-67

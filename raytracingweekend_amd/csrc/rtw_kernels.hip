@@ -131,6 +131,8 @@ struct job_t {
 // records are read back only by k_reduce after the launch, so they stream
 // past the L2 instead of evicting the lines the traversal reuses (scene,
 // nodes beyond the LDS packet, spill slots).
+// Measured (1 MI355X, A/B, profiles/r05/ab_r5b_*.log): T 4 463 vs 4 465,
+// C5 slice 663.7 vs 663.3 -- the records cost the L2 nothing measurable.  Off.
 #ifndef RTW_NT_RECORDS
 #define RTW_NT_RECORDS 0
 #endif

@@ -27,7 +27,7 @@ VARIANTS = {
     "compiler_sqrt": T + ["-DRTW_SQRT_CORE=0"],
     "nt_records": T + ["-DRTW_NT_RECORDS=1"],
     "nt_records_fast": FAST5 + ["-DRTW_NT_RECORDS=1"],
-    "sqrt_core_no_normalize": C5 + ["-DRTW_SQRT_NORM=0"],
+    "sqrt_core_normalize": C5 + ["-DRTW_SQRT_NORM=1"],
     "sort_home_ray": T + ["-DRTW_SORT_HOME_RAY=1"],
     "div3_shared": T + ["-DRTW_DIV3_SHARED=1"],
     "pixel_major": T + ["-DRTW_PIXEL_MAJOR=1"],
