@@ -2501,8 +2501,20 @@ RTW_D double schlick_r0(double cosine, double r0) { return r0 + (1 - r0) * pow5(
 #ifndef RTW_DISK_FP32
 #define RTW_DISK_FP32 RTW_RIUS_FP32
 #endif
+// RTW_PIN_RAYGEN: a pinhole camera (lens_radius 0, no zero origin
+// coordinate) draws the disk point only to advance the engine: rd = 0 * p is
+// a signed zero, so origin + offset == origin, and (x - origin) - offset ==
+// x - origin (that difference is never -0: x - origin is exactly zero only
+// for x == origin != 0, which rounds to +0) -- the point is not formed and
+// the offset not computed.  The draws, the time and the ray are the
+// reference's (camera.h:36-50).
+#ifndef RTW_PIN_RAYGEN
+#define RTW_PIN_RAYGEN 1
+#endif
 RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng) {
     d3 p;
+    const bool pin = RTW_PIN_RAYGEN && c.lens_radius == 0.0 && c.origin[0] != 0.0 && c.origin[1] != 0.0 &&
+                     c.origin[2] != 0.0;  // wave-uniform: the camera is
 #if RTW_DISK_FP32
     {
         constexpr float k2Rf = (float)(2.0 / kCanonR);
@@ -2523,7 +2535,7 @@ RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng
             const d3 q = exact(y1, y2, x1, x2);
             if (dot(q, q) < 1.0) break;
         }
-        p = exact(y1, y2, x1, x2);
+        if (!pin) p = exact(y1, y2, x1, x2);
     }
 #else
     do {
@@ -2532,6 +2544,11 @@ RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng
         p = d3{x, y, 0} * 2.0 - d3{1, 1, 0};
     } while (dot(p, p) >= 1.0);
 #endif
+    if (pin) {
+        const double time = c.time0 + rnd01(rng) * (c.time1 - c.time0);
+        const d3 dir = ld3(c.lower_left) + ld3(c.horizontal) * s + ld3(c.vertical) * t - ld3(c.origin);
+        return ray{ld3(c.origin), normalize(dir), time};
+    }
     const d3 rd = p * c.lens_radius;
     const d3 offset = ld3(c.u) * rd.x + ld3(c.v) * rd.y;
     const double time = c.time0 + rnd01(rng) * (c.time1 - c.time0);
