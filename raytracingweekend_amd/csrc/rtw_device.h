@@ -210,6 +210,24 @@ RTW_D uint32_t mr_next(uint32_t& s) {
     return r;
 }
 
+// The engine k steps ahead: x <- (48271^k mod m) x mod m, one multiply and
+// the same fold as mr_next (a product of two values below 2^31 folds to below
+// 2m, so one conditional subtract finishes it).  RTW_RNG_JUMP: the fp32-decided
+// rejection loops below test only the even draws of a try (the canonical
+// draws' leading terms), so a try jumps two draws at a time and the odd draws
+// are formed only where a try needs its exact fp64 point.
+#ifndef RTW_RNG_JUMP
+#define RTW_RNG_JUMP 1
+#endif
+constexpr uint32_t kMrA = 48271u;
+constexpr uint32_t kMrA2 = 182605794u;  // 48271^2 mod (2^31 - 1)
+RTW_D uint32_t mr_jump(uint32_t s, uint32_t c) {
+    const uint64_t p = (uint64_t)s * c;
+    uint32_t r = (uint32_t)(p & 0x7fffffffu) + (uint32_t)(p >> 31);
+    if (r >= 0x7fffffffu) r -= 0x7fffffffu;
+    return r;
+}
+
 // libstdc++ generate_canonical<double,53>(minstd_rand): two raw draws.
 RTW_D double canon_raw(uint32_t r1, uint32_t r2) {
     const double e1 = (double)(r1 - 1u);
@@ -272,6 +290,24 @@ RTW_D d3 random_in_unit_sphere(uint32_t& s) {
         return d3{x, y, z} * 2.0 - d3{1.0, 1.0, 1.0};
     };
     uint32_t z1, z2, y1, y2, x1, x2;
+#if RTW_RNG_JUMP
+    // a try is draws 1..6 from s0: the even ones by two-step jumps, the odd
+    // ones (z1 = a s0, y1 = a z2, x1 = a y2) only where the point is formed
+    uint32_t s0;
+    for (;;) {
+        s0 = s;
+        z2 = mr_jump(s0, kMrA2), y2 = mr_jump(z2, kMrA2), x2 = mr_jump(y2, kMrA2);
+        s = x2;
+        const float px = lead(x2), py = lead(y2), pz = lead(z2);
+        const float d32 = __builtin_fmaf(px, px, __builtin_fmaf(py, py, pz * pz));
+        if (d32 < 1.0f - 0x1p-14f) break;
+        if (!(d32 < 1.0f + 0x1p-14f)) continue;
+        z1 = mr_jump(s0, kMrA), y1 = mr_jump(z2, kMrA), x1 = mr_jump(y2, kMrA);
+        const d3 q = exact(z1, z2, y1, y2, x1, x2);
+        if (dot(q, q) < 1.0) break;
+    }
+    z1 = mr_jump(s0, kMrA), y1 = mr_jump(z2, kMrA), x1 = mr_jump(y2, kMrA);
+#else
     for (;;) {
         z1 = mr_next(s), z2 = mr_next(s);
         y1 = mr_next(s), y2 = mr_next(s);
@@ -283,6 +319,7 @@ RTW_D d3 random_in_unit_sphere(uint32_t& s) {
         const d3 q = exact(z1, z2, y1, y2, x1, x2);
         if (dot(q, q) < 1.0) break;
     }
+#endif
     return exact(z1, z2, y1, y2, x1, x2);
 #else
     d3 p;
@@ -1477,7 +1514,15 @@ RTW_D bvh_node32 node_at(const scene& S, int i) {
     return decode16(a.x, a.y, a.z, a.w);
 #else
     v4u a, b;
-    if (i < S.n_lnodes) {
+#ifndef RTW_PACKET_ALL
+#define RTW_PACKET_ALL 1
+#endif
+    if (RTW_PACKET_ALL && S.n_lnodes >= S.n_nodes) {
+        // every node is in the packet (wave-uniform: a scalar branch, no
+        // per-lane address-space test; Book 2's 1 668 nodes with F_PIN)
+        lds_v4* p = (lds_v4*)(S.lnodes + i);
+        a = p[0], b = p[1];
+    } else if (i < S.n_lnodes) {
         lds_v4* p = (lds_v4*)(S.lnodes + i);
         a = p[0], b = p[1];
     } else {
@@ -2525,6 +2570,27 @@ RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng
             return d3{x, y, 0} * 2.0 - d3{1, 1, 0};
         };
         uint32_t y1, y2, x1, x2;
+#if RTW_RNG_JUMP
+        // draws 1..4 of a try from s0: y2, x2 by two-step jumps, y1 = a s0 and
+        // x1 = a y2 only where the point is formed (never for a pinhole)
+        uint32_t s0;
+        for (;;) {
+            s0 = rng;
+            y2 = mr_jump(s0, kMrA2), x2 = mr_jump(y2, kMrA2);
+            rng = x2;
+            const float px = lead(x2), py = lead(y2);
+            const float d32 = __builtin_fmaf(px, px, py * py);
+            if (d32 < 1.0f - 0x1p-14f) break;
+            if (!(d32 < 1.0f + 0x1p-14f)) continue;
+            y1 = mr_jump(s0, kMrA), x1 = mr_jump(y2, kMrA);
+            const d3 q = exact(y1, y2, x1, x2);
+            if (dot(q, q) < 1.0) break;
+        }
+        if (!pin) {
+            y1 = mr_jump(s0, kMrA), x1 = mr_jump(y2, kMrA);
+            p = exact(y1, y2, x1, x2);
+        }
+#else
         for (;;) {
             y1 = mr_next(rng), y2 = mr_next(rng);
             x1 = mr_next(rng), x2 = mr_next(rng);
@@ -2536,6 +2602,7 @@ RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng
             if (dot(q, q) < 1.0) break;
         }
         if (!pin) p = exact(y1, y2, x1, x2);
+#endif
     }
 #else
     do {
