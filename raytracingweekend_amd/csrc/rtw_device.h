@@ -398,7 +398,7 @@ struct dev_entry {
     int32_t n_outer_ops;  // MEDIUM: ops enclosing the medium (rtw_entry::n_outer_ops)
     int32_t movers;       // the group holds DP_MOVING_COMMON* spheres
     int32_t bvh_root4;    // its BVH as 4-wide nodes (scene::nodes4), -1 none
-    double density;
+    double neg_inv_density;  // MEDIUM: -(1 / density) (hittable.h:451), IEEE on the host at upload
 };
 struct dev_op {
     int32_t type, pad;
@@ -2067,7 +2067,7 @@ RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_mi
     if (t1 < 0) t1 = 0;
     const double dl = len(r.d);
     const double inside = (t2 - t1) * dl;
-    const double hit_distance = -(1 / rd<true>(&e.p->density)) * log_dev(rnd01(rng));
+    const double hit_distance = rd<true>(&e.p->neg_inv_density) * log_dev(rnd01(rng));
     if (hit_distance < inside) {
         t_out = t1 + hit_distance / dl;
         return true;

@@ -2600,7 +2600,9 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         D.phase_material = E.phase_material, D.bvh_root = E.bvh_root, D.n_outer_ops = E.n_outer_ops;
         D.movers = entry_movers[e];
         D.bvh_root4 = (bvh4_ok && E.bvh_root >= 0) ? root4_of[E.bvh_root] : -1;
-        D.density = E.density;
+        // the reference's -(1 / density), once per upload (a correctly
+        // rounded division and a negation, as on the device)
+        D.neg_inv_density = E.kind == RTW_ENTRY_MEDIUM ? -(1.0 / E.density) : 0.0;
         for (int k = 0; k < E.n_ops; ++k) {
             dev_op o;
             std::memset(&o, 0, sizeof o);
@@ -2792,7 +2794,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             o.first_op = D.first_op, o.phase_material = D.phase_material;
             o.bvh_root = bvh_ok ? D.bvh_root : -1;
             o.n_outer_ops = D.n_outer_ops;
-            o.neg_inv_density = (float)(-(1.0 / D.density));
+            o.neg_inv_density = (float)D.neg_inv_density;
         }
         std::vector<op32> o32(std::max<size_t>(dev_ops.size(), 1));
         for (size_t k = 0; k < dev_ops.size(); ++k) {

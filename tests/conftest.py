@@ -22,17 +22,13 @@ def built():
     compiling.  A library older than its sources is reported, not rebuilt
     (measurements key on the library's own build id).  The oracle (gcc,
     seconds) is made if missing."""
-    from raytracingweekend_amd import build
-    if not build.LIB.exists():
-        pytest.fail(f"{build.LIB} is missing: run `python -m raytracingweekend_amd.build` first")
-    try:
-        import ctypes
-        lib = ctypes.CDLL(str(build.LIB))
-        lib.rtw_build_id.restype = ctypes.c_char_p
-        have, want = lib.rtw_build_id().decode(), build.build_id()
-        if have != want:
-            print(f"\nnote: {build.LIB.name} build id {have} != sources {want} (rebuild to test the sources)")
-    except OSError:
-        pass
+    from raytracingweekend_amd import _abi, build
+    if not _abi.LIB_PATH.exists():
+        pytest.fail(f"{_abi.LIB_PATH} is missing: run `python -m raytracingweekend_amd.build` first")
+    # through _abi: torch's HIP runtime is loaded before the library's (the
+    # other order breaks torch's GPU initialisation later in the session)
+    have = _abi.lib().rtw_build_id().decode()
+    if _abi.LIB_PATH == build.LIB and have != build.build_id():
+        print(f"\nnote: {build.LIB.name} build id {have} != sources {build.build_id()} (rebuild to test the sources)")
     build.build_oracle()
     return True

@@ -65,3 +65,26 @@ def test_lead_term_bound_and_decisions():
     acc2 = d2_32 < np.float32(1.0 - 2.0**-14)
     rej2 = ~(d2_32 < np.float32(1.0 + 2.0**-14))
     assert np.all(d2[acc2] < 1.0) and np.all(d2[rej2] >= 1.0)
+
+
+def test_two_step_jumps_are_the_engine():
+    """RTW_RNG_JUMP (rtw_device.h mr_jump): x -> (48271^2 mod m) x mod m with
+    the Mersenne fold equals two minstd_rand steps, and the odd draw of a
+    pair is 48271 x of the state before it -- on random and edge states; the
+    fold's sum stays below 2m, so one conditional subtract completes it."""
+    m = 2**31 - 1
+    a = 48271
+    a2 = 182605794
+    assert a2 == a * a % m
+
+    def fold(p):  # the device's mr_jump / mr_next on a product below 2^62
+        r = (p & 0x7FFFFFFF) + (p >> 31)
+        assert r < 2 * m
+        return r - m if r >= m else r
+
+    rng = np.random.default_rng(5)
+    states = [1, 2, m - 1, m - 2, 2**30, 48271, a2] + [int(v) for v in rng.integers(1, m, size=20000)]
+    for s in states:
+        one = s * a % m
+        two = one * a % m
+        assert fold(s * a2) == two and fold(s * a) == one
