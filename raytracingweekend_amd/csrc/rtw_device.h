@@ -216,6 +216,9 @@ RTW_D uint32_t mr_next(uint32_t& s) {
 // rejection loops below test only the even draws of a try (the canonical
 // draws' leading terms), so a try jumps two draws at a time and the odd draws
 // are formed only where a try needs its exact fp64 point.
+// Measured (1 MI355X, A/B, profiles/r05/ab_r5c_*.log): T 4 607 vs 4 574,
+// C3 slice 3 058 vs 3 017, C2 2 258 vs 2 242, C5 ±0 alone (+4 % with
+// RTW_PACKET_ALL, below).
 #ifndef RTW_RNG_JUMP
 #define RTW_RNG_JUMP 1
 #endif
@@ -1514,6 +1517,8 @@ RTW_D bvh_node32 node_at(const scene& S, int i) {
     return decode16(a.x, a.y, a.z, a.w);
 #else
     v4u a, b;
+// Measured (1 MI355X, A/B, profiles/r05/ab_r5c_*.log): C5 slice 691 vs 675
+// alone, 703 with RTW_RNG_JUMP; C3 3 148 vs 3 058 with it; T ±0.
 #ifndef RTW_PACKET_ALL
 #define RTW_PACKET_ALL 1
 #endif
