@@ -159,6 +159,14 @@ __device__ __forceinline__ double rad_div(double a, double b) {
 }
 RTW_HD double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RTW_HD double len2(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+// RTW_PACKET_ALL: node_at reads the LDS packet without a per-lane
+// address-space test when every node of the scene is in it (a wave-uniform
+// test of the packet size; fp64 and fp32 walks).  Measured (1 MI355X, A/B,
+// profiles/r05/ab_r5c_*.log): C5 slice 691 vs 675 alone, 703 with
+// RTW_RNG_JUMP; C3 3 148 vs 3 058 with it; T ±0.
+#ifndef RTW_PACKET_ALL
+#define RTW_PACKET_ALL 1
+#endif
 // RTW_SQRT_CORE: fp64 square roots as rtw_div.h's sqrt_w (the compiler's own
 // sequence without its range scaling and class fixup, taken when the whole
 // wave is in range; bit for bit the same value) or sqrt_core where the range
@@ -1517,11 +1525,6 @@ RTW_D bvh_node32 node_at(const scene& S, int i) {
     return decode16(a.x, a.y, a.z, a.w);
 #else
     v4u a, b;
-// Measured (1 MI355X, A/B, profiles/r05/ab_r5c_*.log): C5 slice 691 vs 675
-// alone, 703 with RTW_RNG_JUMP; C3 3 148 vs 3 058 with it; T ±0.
-#ifndef RTW_PACKET_ALL
-#define RTW_PACKET_ALL 1
-#endif
     if (RTW_PACKET_ALL && S.n_lnodes >= S.n_nodes) {
         // every node is in the packet (wave-uniform: a scalar branch, no
         // per-lane address-space test; Book 2's 1 668 nodes with F_PIN)

@@ -377,7 +377,10 @@ RTW_D bvh_node32 node_at(const fscene& S, int i) {
     return rtwd::decode16(a.x, a.y, a.z, a.w);
 #else
     v4u a, b;
-    if (i < S.n_lnodes) {
+    if (RTW_PACKET_ALL && S.n_lnodes >= S.n_nodes) {  // every node in the packet: wave-uniform
+        lds_v4* p = (lds_v4*)(S.lnodes + i);
+        a = p[0], b = p[1];
+    } else if (i < S.n_lnodes) {
         lds_v4* p = (lds_v4*)(S.lnodes + i);
         a = p[0], b = p[1];
     } else {
