@@ -18,6 +18,3 @@ tail -n 1 gpurun_out/bench_T_$tag.txt | cut -c1-300
 bash scripts/bench_configs.sh $tag > /dev/null
 bash scripts/bench_fp32.sh $tag > /dev/null
 bash scripts/full_configs.sh $tag > /dev/null
-# A/B: the pinhole ray generation shortcut (in-tree) against librtw_nopinrg
-bash scripts/ab_libs.sh r5e_pin 3 "--workload T" default raytracingweekend_amd/_build/librtw_nopinrg.so
-bash scripts/ab_libs.sh r5e_pin 2 "--workload C5 --spp 64" default raytracingweekend_amd/_build/librtw_nopinrg.so
