@@ -1627,6 +1627,10 @@ RTW_D void push_children(const bvh_node32& nd, int dneg, STK& stk, int& sp) {
 #define RTW_SPEC_WALK 1
 #endif
 // ... and for the group BVH walks (while-while form)
+// RTW_GROUP_TOS: the group walks keep the nearer child in a register (below)
+#ifndef RTW_GROUP_TOS
+#define RTW_GROUP_TOS 1
+#endif
 #ifndef RTW_SPEC_GROUP
 #define RTW_SPEC_GROUP 0
 #endif
@@ -1880,6 +1884,34 @@ RTW_D void group_bvh(const scene& S, int root, int root4, const ray& r, double t
         }
         if (__builtin_amdgcn_ballot_w64(lc != 0) == 0) break;
         for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
+    }
+#elif RTW_GROUP_TOS
+    // top of stack in a register: an inner node's nearer child is the next
+    // node to visit, so it is kept in `next` instead of being pushed and
+    // popped again at once through the LDS stack (only the farther child is
+    // stored); the visiting order is unchanged
+    --sp;  // the root is `next`, not a stack entry
+    int next = root;
+    bool have = true;
+    for (;;) {
+        int la = 0, lc = 0;
+        while (lc == 0 && (have || sp > base)) {
+            const int ni = have ? next : stk.at(--sp);
+            have = false;
+            const bvh_node32 nd = node_at(S, ni);
+            if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
+            lc = node_count(nd);
+            la = nd.a;
+            if (lc == 0 && sp + 1 <= STK::cap) {  // always true: depth checked at upload
+                const int pad = nd.b >> 28, right = nd.b & 0x0fffffff;
+                const bool left_first = (((dneg >> (pad & 3)) ^ (pad >> 2)) & 1) == 0;
+                stk.at(sp++) = left_first ? right : nd.a;
+                next = left_first ? nd.a : right;
+                have = true;
+            }
+        }
+        if (lc == 0) break;
+        leaf_items(S, la, lc, r, t_min, h, fc);
     }
 #else
     for (;;) {

@@ -364,6 +364,11 @@ RTW_D bool slab(const bvh_node32& nd, const slab_rayf& s, float t0, float t1) {
 }
 // (explicit address spaces, as rtwd::node_at: an LDS read for packet nodes,
 // a global read for the rest)
+// PALL: the all-in-packet shortcut (RTW_PACKET_ALL) is compiled in; the
+// media kernel leaves it out (its packet never holds every node at two
+// workgroups per CU, and the branch cost it a spilled register: C5 fp32
+// -1.4 %, profiles/r05/ab_r5f_fpall.log)
+template <bool PALL = true>
 RTW_D bvh_node32 node_at(const fscene& S, int i) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     using lds_v4 = const __attribute__((address_space(3))) v4u;
@@ -377,7 +382,7 @@ RTW_D bvh_node32 node_at(const fscene& S, int i) {
     return rtwd::decode16(a.x, a.y, a.z, a.w);
 #else
     v4u a, b;
-    if (RTW_PACKET_ALL && S.n_lnodes >= S.n_nodes) {  // every node in the packet: wave-uniform
+    if (PALL && RTW_PACKET_ALL && S.n_lnodes >= S.n_nodes) {  // every node in the packet: wave-uniform
         lds_v4* p = (lds_v4*)(S.lnodes + i);
         a = p[0], b = p[1];
     } else if (i < S.n_lnodes) {
@@ -424,14 +429,33 @@ struct priv_stackf {
     RTW_D int& at(int i) { return s[i]; }
 };
 
-template <class STK>
+template <bool PALL = true, class STK>
 RTW_D void group_bvh(const fscene& S, int root, const fray& r, float tmin, fhit& h, STK& stk, int base) {
     const slab_rayf sr = make_slab(S, r);
     const float t0 = tmin > 0 ? tmin * 0.5f : tmin * 2.0f - 1e-6f;
     int sp = base;
+#if RTW_GROUP_TOS
+    // the next node (the left child of the node just expanded) in a
+    // register, only the right one through the stack: the order is unchanged
+    int next = root;
+    bool have = true;
+    while (have || sp > base) {
+        const int ni = have ? next : stk.at(--sp);
+        have = false;
+        const bvh_node32 nd = node_at<PALL>(S, ni);
+        if (!slab(nd, sr, t0, h.t)) continue;
+        if (nd.b < 0) {
+            for (int k = 0; k < -nd.b; ++k) arbitrate_item(S, S.items[nd.a + k], r, tmin, h);
+        } else if (sp + 1 <= STK::cap) {
+            stk.at(sp++) = nd.b & 0x0fffffff;
+            next = nd.a;
+            have = true;
+        }
+    }
+#else
     stk.at(sp++) = root;
     while (sp > base) {
-        const bvh_node32 nd = node_at(S, stk.at(--sp));
+        const bvh_node32 nd = node_at<PALL>(S, stk.at(--sp));
         if (!slab(nd, sr, t0, h.t)) continue;
         if (nd.b < 0) {
             for (int k = 0; k < -nd.b; ++k) arbitrate_item(S, S.items[nd.a + k], r, tmin, h);
@@ -440,12 +464,13 @@ RTW_D void group_bvh(const fscene& S, int root, const fray& r, float tmin, fhit&
             stk.at(sp++) = nd.a;
         }
     }
+#endif
 }
 
 template <int F, class STK>
 RTW_D void group_closest(const fscene& S, const ent_v& e, const fray& r, float tmin, fhit& h, STK& stk, int base) {
     if ((F & rtwd::F_GBVH) && e.bvh_root >= 0)
-        group_bvh(S, e.bvh_root, r, tmin, h, stk, base);
+        group_bvh<(F & rtwd::F_MEDIA) == 0>(S, e.bvh_root, r, tmin, h, stk, base);
     else
         group_scan(S, e.first_prim, e.n_prims, r, tmin, h);
 }
@@ -499,7 +524,7 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 if (__builtin_amdgcn_ballot_w64(lc == 0 && sp > 0) == 0) break;
                 if (sp == 0 || stall) continue;
                 const int ni = stk.at(--sp);
-                const bvh_node32 nd = node_at(S, ni);
+                const bvh_node32 nd = node_at<(F & rtwd::F_MEDIA) == 0>(S, ni);
                 if (!slab(nd, sr, t0, h.t)) continue;
                 if (nd.b >= 0) {
                     if (sp + 2 <= STK::cap) stk.at(sp++) = nd.b & 0x0fffffff, stk.at(sp++) = nd.a;
@@ -520,20 +545,34 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 const ent_v e = view_entry<false>(S, it);
                 const fray lr = ops_in<false>(e, r, 0, e.n_ops);
                 if ((F & rtwd::F_GBVH) && e.bvh_root >= 0)
-                    group_bvh(S, e.bvh_root, lr, kTMinF, h, stk, sp);
+                    group_bvh<(F & rtwd::F_MEDIA) == 0>(S, e.bvh_root, lr, kTMinF, h, stk, sp);
                 else
                     for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMinF, h);
             }
         }
         if (false)
 #endif
+#if RTW_GROUP_TOS
+        // the next node in a register (group_bvh's form): the root, then the
+        // left child of each node expanded; only right children are stacked
+        for (int next = (sp = 0, S.world_bvh_root), have = 1; have || sp > 0;) {
+            const int ni = have ? next : stk.at(--sp);
+            have = 0;
+            const bvh_node32 nd = node_at<(F & rtwd::F_MEDIA) == 0>(S, ni);
+            if (!slab(nd, sr, t0, h.t)) continue;
+            if (nd.b >= 0) {
+                if (sp + 1 <= STK::cap) stk.at(sp++) = nd.b & 0x0fffffff, next = nd.a, have = 1;
+                continue;
+            }
+#else
         while (sp > 0) {
-            const bvh_node32 nd = node_at(S, stk.at(--sp));
+            const bvh_node32 nd = node_at<(F & rtwd::F_MEDIA) == 0>(S, stk.at(--sp));
             if (!slab(nd, sr, t0, h.t)) continue;
             if (nd.b >= 0) {
                 if (sp + 2 <= STK::cap) stk.at(sp++) = nd.b & 0x0fffffff, stk.at(sp++) = nd.a;
                 continue;
             }
+#endif
             for (int k = 0; k < -nd.b; ++k) {
                 const int it = S.items[nd.a + k];
                 if (it < 0) {  // a plain one-prim entry: ~prim
@@ -543,7 +582,7 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 const ent_v e = view_entry<false>(S, it);
                 const fray lr = ops_in<false>(e, r, 0, e.n_ops);
                 if ((F & rtwd::F_GBVH) && e.bvh_root >= 0)
-                    group_bvh(S, e.bvh_root, lr, kTMinF, h, stk, sp);
+                    group_bvh<(F & rtwd::F_MEDIA) == 0>(S, e.bvh_root, lr, kTMinF, h, stk, sp);
                 else
                     for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMinF, h);
             }
@@ -576,7 +615,7 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 const ent_v e = view_entry<true>(S, ei);
                 const fray lr = ops_in<true>(e, r, 0, e.n_ops);
                 if ((F & rtwd::F_GBVH) && e.bvh_root >= 0) {
-                    group_bvh(S, e.bvh_root, lr, kTMinF, h, stk, 0);
+                    group_bvh<(F & rtwd::F_MEDIA) == 0>(S, e.bvh_root, lr, kTMinF, h, stk, 0);
                     continue;
                 }
                 group_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), lr, kTMinF, h);
