@@ -1627,9 +1627,14 @@ RTW_D void push_children(const bvh_node32& nd, int dneg, STK& stk, int& sp) {
 #define RTW_SPEC_WALK 1
 #endif
 // ... and for the group BVH walks (while-while form)
-// RTW_GROUP_TOS: the group walks keep the nearer child in a register (below)
+// RTW_GROUP_TOS: the group walks keep the nearer child in a register instead
+// of pushing and popping it through the LDS stack (below; rtw_fast.h's group
+// and world walks likewise).  Measured (1 MI355X, A/B,
+// profiles/r05/ab_r5d_*.log): C5 slice 671 vs 709, C3 fp32 4 652 vs 5 191,
+// C5 fp32 812 vs 846 -- the per-lane select between register and stack and
+// the masked stack read cost more than the LDS round trip.  Off.
 #ifndef RTW_GROUP_TOS
-#define RTW_GROUP_TOS 1
+#define RTW_GROUP_TOS 0
 #endif
 #ifndef RTW_SPEC_GROUP
 #define RTW_SPEC_GROUP 0

@@ -26,6 +26,9 @@ VARIANTS = {
     "canon_two_steps": T + ["-DRTW_CANON_ONESTEP=0"],
     "compiler_sqrt": T + ["-DRTW_SQRT_CORE=0"],
     "nt_records": T + ["-DRTW_NT_RECORDS=1"],
+    "group_tos": C5 + ["-DRTW_GROUP_TOS=1"],
+    "group_tos_fast": FAST5 + ["-DRTW_GROUP_TOS=1"],
+    "no_rng_jump": T + ["-DRTW_RNG_JUMP=0", "-DRTW_PACKET_ALL=0"],
     "nt_records_fast": FAST5 + ["-DRTW_NT_RECORDS=1"],
     "sqrt_core_normalize": C5 + ["-DRTW_SQRT_NORM=1"],
     "sort_home_ray": T + ["-DRTW_SORT_HOME_RAY=1"],
