@@ -415,14 +415,30 @@ RTW_D bvh_node32 node_at(const fscene& S, int i) {
 #define RTW_FAST_BLOCK 1024
 #endif
 constexpr int kFastBlock = RTW_FAST_BLOCK;
+// ... and of the media kernel (F_MEDIA: Book 2), with its waves per SIMD
+// (rtw_kernels.hip k_fast): 896 threads at 7 waves = two workgroups of 14
+// waves per CU, 72 VGPRs a wave
+#ifndef RTW_FAST_MEDIA_BLOCK
+#define RTW_FAST_MEDIA_BLOCK 1024
+#endif
+constexpr int fast_block(int F) { return (F & rtwd::F_MEDIA) ? RTW_FAST_MEDIA_BLOCK : kFastBlock; }
+// the all-in-packet node fetch (node_at<PALL>): compiled into the media
+// kernel only with RTW_FAST_MEDIA_PALL (its packet holds every node only at
+// smaller workgroups)
+#ifndef RTW_FAST_MEDIA_PALL
+#define RTW_FAST_MEDIA_PALL 0
+#endif
+constexpr bool fast_pall(int F) { return (F & rtwd::F_MEDIA) == 0 || RTW_FAST_MEDIA_PALL; }
 
-// traversal stacks: a column of 16-bit node ids per lane in LDS, or a
-// private array
-struct lds_stackf {
+// traversal stacks: a column of 16-bit node ids per lane in LDS (column
+// stride: the workgroup size), or a private array
+template <int BLK>
+struct lds_stackf_t {
     static constexpr int cap = rtwd::kLdsStack;
     uint16_t* p;
-    RTW_D uint16_t& at(int i) { return p[i * kFastBlock]; }
+    RTW_D uint16_t& at(int i) { return p[i * BLK]; }
 };
+using lds_stackf = lds_stackf_t<kFastBlock>;
 struct priv_stackf {
     static constexpr int cap = rtwd::kStack;
     int s[rtwd::kStack];
@@ -470,7 +486,7 @@ RTW_D void group_bvh(const fscene& S, int root, const fray& r, float tmin, fhit&
 template <int F, class STK>
 RTW_D void group_closest(const fscene& S, const ent_v& e, const fray& r, float tmin, fhit& h, STK& stk, int base) {
     if ((F & rtwd::F_GBVH) && e.bvh_root >= 0)
-        group_bvh<(F & rtwd::F_MEDIA) == 0>(S, e.bvh_root, r, tmin, h, stk, base);
+        group_bvh<fast_pall(F)>(S, e.bvh_root, r, tmin, h, stk, base);
     else
         group_scan(S, e.first_prim, e.n_prims, r, tmin, h);
 }
@@ -524,7 +540,7 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 if (__builtin_amdgcn_ballot_w64(lc == 0 && sp > 0) == 0) break;
                 if (sp == 0 || stall) continue;
                 const int ni = stk.at(--sp);
-                const bvh_node32 nd = node_at<(F & rtwd::F_MEDIA) == 0>(S, ni);
+                const bvh_node32 nd = node_at<fast_pall(F)>(S, ni);
                 if (!slab(nd, sr, t0, h.t)) continue;
                 if (nd.b >= 0) {
                     if (sp + 2 <= STK::cap) stk.at(sp++) = nd.b & 0x0fffffff, stk.at(sp++) = nd.a;
@@ -545,7 +561,7 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 const ent_v e = view_entry<false>(S, it);
                 const fray lr = ops_in<false>(e, r, 0, e.n_ops);
                 if ((F & rtwd::F_GBVH) && e.bvh_root >= 0)
-                    group_bvh<(F & rtwd::F_MEDIA) == 0>(S, e.bvh_root, lr, kTMinF, h, stk, sp);
+                    group_bvh<fast_pall(F)>(S, e.bvh_root, lr, kTMinF, h, stk, sp);
                 else
                     for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMinF, h);
             }
@@ -558,7 +574,7 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
         for (int next = (sp = 0, S.world_bvh_root), have = 1; have || sp > 0;) {
             const int ni = have ? next : stk.at(--sp);
             have = 0;
-            const bvh_node32 nd = node_at<(F & rtwd::F_MEDIA) == 0>(S, ni);
+            const bvh_node32 nd = node_at<fast_pall(F)>(S, ni);
             if (!slab(nd, sr, t0, h.t)) continue;
             if (nd.b >= 0) {
                 if (sp + 1 <= STK::cap) stk.at(sp++) = nd.b & 0x0fffffff, next = nd.a, have = 1;
@@ -566,7 +582,7 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
             }
 #else
         while (sp > 0) {
-            const bvh_node32 nd = node_at<(F & rtwd::F_MEDIA) == 0>(S, stk.at(--sp));
+            const bvh_node32 nd = node_at<fast_pall(F)>(S, stk.at(--sp));
             if (!slab(nd, sr, t0, h.t)) continue;
             if (nd.b >= 0) {
                 if (sp + 2 <= STK::cap) stk.at(sp++) = nd.b & 0x0fffffff, stk.at(sp++) = nd.a;
@@ -582,7 +598,7 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 const ent_v e = view_entry<false>(S, it);
                 const fray lr = ops_in<false>(e, r, 0, e.n_ops);
                 if ((F & rtwd::F_GBVH) && e.bvh_root >= 0)
-                    group_bvh<(F & rtwd::F_MEDIA) == 0>(S, e.bvh_root, lr, kTMinF, h, stk, sp);
+                    group_bvh<fast_pall(F)>(S, e.bvh_root, lr, kTMinF, h, stk, sp);
                 else
                     for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMinF, h);
             }
@@ -615,7 +631,7 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 const ent_v e = view_entry<true>(S, ei);
                 const fray lr = ops_in<true>(e, r, 0, e.n_ops);
                 if ((F & rtwd::F_GBVH) && e.bvh_root >= 0) {
-                    group_bvh<(F & rtwd::F_MEDIA) == 0>(S, e.bvh_root, lr, kTMinF, h, stk, 0);
+                    group_bvh<fast_pall(F)>(S, e.bvh_root, lr, kTMinF, h, stk, 0);
                     continue;
                 }
                 group_scan(S, ld(&S.runs[ri].first_prim), ld(&S.runs[ri].n_prims), lr, kTMinF, h);

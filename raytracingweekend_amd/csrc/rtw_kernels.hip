@@ -1450,6 +1450,10 @@ constexpr int FF_NONOISE = 1 << 12;
 #ifndef RTW_FAST_BVH_WAVES
 #define RTW_FAST_BVH_WAVES 8
 #endif
+#ifndef RTW_FAST_MEDIA_WAVES
+#define RTW_FAST_MEDIA_WAVES RTW_FAST_BVH_WAVES
+#endif
+#define RTW_FAST_WAVES_OF(F) (((F) & F_MEDIA) ? RTW_FAST_MEDIA_WAVES : RTW_FAST_BVH_WAVES)
 // HOME (RTW_FAST_HOME(F)): the path's throughput and sample id wait in the
 // lane's LDS home slots instead of registers (k_persist's plan), and the
 // segments are counted per wave in a scalar register -- the loop-carried
@@ -1458,22 +1462,23 @@ constexpr int FF_NONOISE = 1 << 12;
 #define RTW_FAST_HOME(F) 0
 #endif
 template <int F, bool LST>
-__global__ __launch_bounds__(rtwf::kFastBlock) __attribute__((amdgpu_waves_per_eu(RTW_FAST_BVH_WAVES)))
+__global__ __launch_bounds__(rtwf::fast_block(F)) __attribute__((amdgpu_waves_per_eu(RTW_FAST_WAVES_OF(F))))
 void k_fast(fast_args) {
     using namespace rtwf;
     constexpr bool NOISE = (F & FF_NONOISE) == 0;
     constexpr bool HOME = RTW_FAST_HOME(F) != 0;
-    constexpr int kFW = kFastBlock / 64;
+    constexpr int kFB = fast_block(F);
+    constexpr int kFW = kFB / 64;
     extern __shared__ __attribute__((aligned(16))) char s_nodes[];
-    __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kFastBlock];
+    __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kFB];
     __shared__ uint32_t s_cnt[kFW];
-    __shared__ float s_thr[HOME ? 3 : 1][HOME ? kFastBlock : 1];
-    __shared__ uint32_t s_q[HOME ? kFastBlock : 1];
+    __shared__ float s_thr[HOME ? 3 : 1][HOME ? kFB : 1];
+    __shared__ uint32_t s_q[HOME ? kFB : 1];
     if (LST) {  // the BVH node packet (the top levels of every tree)
         const fast_args& A = fast_args_now();
         const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
         uint4* dst = reinterpret_cast<uint4*>(s_nodes);
-        for (uint32_t k = threadIdx.x; k < A.lds_nodes * (uint32_t)(sizeof(node_store) / 16); k += kFastBlock)
+        for (uint32_t k = threadIdx.x; k < A.lds_nodes * (uint32_t)(sizeof(node_store) / 16); k += kFB)
             dst[k] = src[k];
         __syncthreads();
     }
@@ -1539,7 +1544,7 @@ void k_fast(fast_args) {
         if (depth == 0) continue;
         fhit h;
         if constexpr (LST) {
-            lds_stackf stk{&s_stack[0][threadIdx.x]};
+            lds_stackf_t<kFB> stk{&s_stack[0][threadIdx.x]};
             const fast_args& A = fast_args_now();
             fscene S = A.S;
             S.lnodes = reinterpret_cast<const node_store*>(s_nodes);
@@ -3131,17 +3136,17 @@ bool launch_persist(bool probe, int f, int mask, int cus, hipStream_t st, const 
 // BVH node packet of a k_fast<.., LST> launch: the most top nodes that fit
 // in LDS beside the stacks without costing a workgroup per CU (node_packet's
 // rule; RTW_LDS_NODES caps it, 0 = off).
-uint32_t fast_node_packet(const void* fn, int n_nodes) {
+uint32_t fast_node_packet(const void* fn, int n_nodes, int block) {
     const char* e = std::getenv("RTW_LDS_NODES");
     uint32_t cap = (e && *e) ? (uint32_t)std::max(0, std::atoi(e)) : 4096u;
     cap = std::min<uint32_t>(cap, (uint32_t)std::max(0, n_nodes));
     if (!cap) return 0;
-    const int base = blocks_per_cu(fn, rtwf::kFastBlock, 0);
+    const int base = blocks_per_cu(fn, block, 0);
     if (base <= 0) return 0;
     uint32_t best = 0;
     for (uint32_t k = 32; k <= cap + 31; k += 32) {
         const uint32_t kk = std::min(k, cap);
-        if (blocks_per_cu(fn, rtwf::kFastBlock, kk * sizeof(node_store)) < base) break;
+        if (blocks_per_cu(fn, block, kk * sizeof(node_store)) < base) break;
         best = kk;
         if (kk == cap) break;
     }
@@ -3157,10 +3162,11 @@ void launch_fast_t(bool probe, std::string* name, int cus, hipStream_t st, const
     if (probe) return;
     const void* fn = reinterpret_cast<const void*>(&k_fast<FF, LST>);
     fast_args a = A;
-    a.lds_nodes = LST ? fast_node_packet(fn, A.S.n_nodes) : 0u;
+    constexpr int blk = rtwf::fast_block(FF);
+    a.lds_nodes = LST ? fast_node_packet(fn, A.S.n_nodes, blk) : 0u;
     const size_t shm = (size_t)a.lds_nodes * sizeof(node_store);
-    const int grid = grid_blocks(fn, rtwf::kFastBlock, shm, cus);
-    hipLaunchKernelGGL((k_fast<FF, LST>), dim3(grid), dim3(rtwf::kFastBlock), shm, st, a);
+    const int grid = grid_blocks(fn, blk, shm, cus);
+    hipLaunchKernelGGL((k_fast<FF, LST>), dim3(grid), dim3(blk), shm, st, a);
 }
 template <int FF, bool LL>
 void launch_fast_sort_t(bool probe, std::string* name, int cus, hipStream_t st, const fast_args& A,
