@@ -416,8 +416,11 @@ RTW_D bvh_node32 node_at(const fscene& S, int i) {
 #endif
 constexpr int kFastBlock = RTW_FAST_BLOCK;
 // ... and of the media kernel (F_MEDIA: Book 2), with its waves per SIMD
-// (rtw_kernels.hip k_fast): 896 threads at 7 waves = two workgroups of 14
-// waves per CU, 72 VGPRs a wave
+// (rtw_kernels.hip RTW_FAST_MEDIA_WAVES).  Measured (1 MI355X, A/B,
+// profiles/r05/ab_r5e_fmedia.log, C5 fp32 slice): 1 024 threads at 8 waves
+// (64 VGPRs, 17 spilled) 843; 896 at 7 (72 VGPRs, 9 spilled, a 1 632-node
+// packet) 472; 768 at 6 (spill-free, every node in the packet, its fetch
+// shortcut) 751.  1 024 stays.
 #ifndef RTW_FAST_MEDIA_BLOCK
 #define RTW_FAST_MEDIA_BLOCK 1024
 #endif
