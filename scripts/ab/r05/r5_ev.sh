@@ -8,3 +8,5 @@ tag=$1
 bash scripts/ab/r05/r5_ev1.sh $tag
 cp gpurun_out/pmc/*_$tag.json profiles/pmc/
 bash scripts/ab/r05/r5_ev2.sh $tag
+# where the lane time goes (the -DRTW_PROF build of the same sources)
+bash scripts/prof_sections.sh
