@@ -2519,8 +2519,9 @@ RTW_D d3 frame_w(const scene& S, const surf_frame& s) {  // == frame_onb(S, s).w
 // (sphere.h:101-108, utility.h:69-81) share their sqrt / sincos / onb tail,
 // so a wave whose lanes took different branches pays for one sincos, not
 // two.  Every lane draws and rounds exactly as its own branch would.
-RTW_D d3 mixture_generate(const scene& S, const surf_frame& sf, d3 o, uint32_t& rng) {
-    const bool cosine = rnd01(rng) < 0.5;
+RTW_D d3 mixture_generate(const scene& S, const surf_frame& sf, d3 o, uint32_t& rng, uint32_t pre = 0) {
+    // (pre: the choice already drawn -- 1 cosine, 2 lights; 0 draws it here)
+    const bool cosine = pre ? pre == 1 : rnd01(rng) < 0.5;
     rtw_light L{RTW_LIGHT_DEFAULT, 0};
     int kind = -1;  // the cosine lobe
     if (!cosine) {

@@ -35,6 +35,7 @@ VARIANTS = {
     "div3_shared": T + ["-DRTW_DIV3_SHARED=1"],
     "pixel_major": T + ["-DRTW_PIXEL_MAJOR=1"],
     "key_order": T + ["-DRTW_KEY_ORDER=2"],
+    "sort_mixture": T + ["-DRTW_SORT_MIXTURE=1"],
     "profiling": T + ["-DRTW_PROF"],
     "bvh4": C3 + ["-DRTW_BVH4=1"],
     "packet": C3 + ["-DRTW_PACKET=1"],
