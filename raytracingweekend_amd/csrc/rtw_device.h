@@ -386,7 +386,8 @@ struct bvh_node16;
 // fp16 operands cost v_fma_mix_f32 at 4.4 cycles per wave instruction, or
 // v_cvt_f32_f16 at 4.3 + v_fma_f32 at 2.75 (converted bounds measured worse:
 // C3 2 582), against 2.75 for v_fma_f32 (profiles/r04/valu_rates_r4f.log).
-// Off; -DRTW_NODE16=1 selects it.
+// Off; -DRTW_NODE16=1 selects it.  (fp32 Book 2, whose 32-B packet misses
+// ~230 nodes: 805 vs 843 Msamples/s, profiles/r05/ab_r5i_node16_fp32_rejected.log)
 #ifndef RTW_NODE16
 #define RTW_NODE16 0
 #endif
