@@ -336,7 +336,9 @@ def result_line(args, world, spp_total, elapsed, samples, seg, ms_gpu, roof, pha
                    "ny": args.ny, "spp_total": spp_total, "spp_per_gpu": spp_total / world,
                    "max_depth": args.depth, "bvh": args.bvh, "precision": args.precision,
                    "global_batch": samples_per_step,
-                   "parallelism": f"spp-shard x{world}" + (" + RCCL reduce" if world > 1 else "")},
+                   "parallelism": f"spp-shard x{world}" + (
+                       (" + gloo reduce (rehearsal: every rank on cuda:0)" if getattr(args, "shared_gpu", False)
+                        else " + RCCL reduce") if world > 1 else "")},
         "msegments_per_s": round(seg / elapsed / 1e6, 2) if seg else None,
         "segments_per_sample": round(seg / max(samples, 1), 4),
         "ms_render_gpu": round(ms_gpu, 3),
@@ -366,15 +368,23 @@ def main():
 
     if not (ROOT / "raytracingweekend_amd" / "librtw.so").exists():
         build.build_library()
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # RTW_BENCH_SHARED_GPU=1: a rehearsal of the N > 1 path on a one-GPU box --
+    # every rank renders on cuda:0 and the collectives run over gloo (RCCL
+    # refuses two ranks on one device).  Its line says so in config.parallelism.
+    args.shared_gpu = world > 1 and os.environ.get("RTW_BENCH_SHARED_GPU", "") == "1"
+    gpu = 0 if args.shared_gpu else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.shared_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     nx, ny, depth = args.nx, args.ny, args.depth
     spp_total = args.spp if args.scaling == "strong" else args.spp * world
     sd = SceneDesc(args.scene, nx / ny, args.bvh)
-    ds = DeviceScene(sd, local_rank)
+    ds = DeviceScene(sd, gpu)
     info = ds.query()
     accum = torch.zeros(nx * ny * 3, dtype=torch.float64, device=dev)
     canvas = torch.zeros_like(accum)
