@@ -2101,9 +2101,6 @@ struct handle_t {
     dev_buf fresh;    // staging of new camera rays (fresh_t)
     dev_buf hits;
     dev_buf radiance; // per-sample planes of one pass
-    dev_buf radiance_x[2];  // overlapped passes (RTW_OVERLAP): the second and third record buffers
-    hipStream_t pstream[2] = {nullptr, nullptr};  // ... the passes' streams (alternating)
-    hipStream_t rstream = nullptr;                // ... and the reductions' stream
     dev_buf run;      // per-pixel running sums
     dev_buf flog;     // RTW_STRICT_RADIANCE: per-thread factor logs (job_t::flog)
     dev_buf accum;    // device accum when the caller passes a host pointer
@@ -3334,25 +3331,6 @@ hipEvent_t event_at(handle_t* h, size_t k) {
     return h->events[k];
 }
 
-// Overlapped passes (persistent forms; RTW_OVERLAP = n > 1 splits a render
-// of at least 2n samples per pixel into n passes): pass i runs on one of two
-// streams with record buffer and queue counters i % 3, and its ordered
-// reduction (k_reduce into the running sums, pass after pass -- the sample
-// order of every pixel's sum is unchanged) runs on a third stream while pass
-// i + 1 traces.  The reduction's waves fit beside the traversal kernel's on
-// each SIMD (k_reduce: 24 VGPRs, no LDS), and pass i + 1's workgroups take
-// the CU slots pass i's tail frees.  Pass i + 3 waits for reduction i (its
-// buffer).  The strict-radiance build keeps one pass at a time (its factor
-// logs are per resident thread).
-#ifndef RTW_OVERLAP_DEFAULT
-#define RTW_OVERLAP_DEFAULT 0
-#endif
-constexpr int kPassCtrs = 3;
-int overlap_passes() {
-    const char* e = std::getenv("RTW_OVERLAP");
-    return (e && *e) ? std::atoi(e) : RTW_OVERLAP_DEFAULT;
-}
-
 size_t pass_budget_samples() {
     if (const char* s = std::getenv("RTW_PASS_SAMPLES")) {
         const long long v = std::atoll(s);
@@ -3507,7 +3485,7 @@ extern "C" int rtw_scene_upload(int device, const rtw_scene_desc* desc, void** o
         return rtw_fail(RTW_ERR_HIP, "hipStreamCreate failed");
     }
     rc = upload_scene(h, desc);
-    if (!rc) rc = h->ctrs.ensure(kPassCtrs * sizeof(ctrs_t));
+    if (!rc) rc = h->ctrs.ensure(sizeof(ctrs_t));
     if (!rc && hipHostMalloc((void**)&h->host_ctrs, sizeof(ctrs_t) * 64, hipHostMallocDefault) != hipSuccess)
         rc = rtw_fail(RTW_ERR_OOM, "hipHostMalloc failed");
     if (rc) {
@@ -3530,8 +3508,6 @@ extern "C" void rtw_scene_free(void* handle) {
     h->fresh.release();
     h->hits.release();
     h->radiance.release();
-    h->radiance_x[0].release();
-    h->radiance_x[1].release();
     h->run.release();
     h->flog.release();
     h->accum.release();
@@ -3539,8 +3515,6 @@ extern "C" void rtw_scene_free(void* handle) {
     h->camera.release();
     if (h->host_ctrs) hipHostFree(h->host_ctrs);
     for (hipEvent_t e : h->events) hipEventDestroy(e);
-    for (hipStream_t x : {h->pstream[0], h->pstream[1], h->rstream})
-        if (x) hipStreamDestroy(x);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -3619,7 +3593,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     ctrs_t* C = static_cast<ctrs_t*>(h->ctrs.p);
     double* run = static_cast<double*>(h->run.p);
     HIPCHK(hipMemsetAsync(run, 0, npix * 24, st));
-    HIPCHK(hipMemsetAsync(C, 0, kPassCtrs * sizeof(ctrs_t), st));
+    HIPCHK(hipMemsetAsync(C, 0, sizeof(ctrs_t), st));
 
     job_t J;
     h->cam_host = *camera;
@@ -3689,90 +3663,47 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
     if (RTW_STRICT_RADIANCE && !persistent)
         return rtw_fail(RTW_ERR_UNSUPPORTED, "the strict-radiance build renders with the persistent kernel only "
                                              "(RTW_MODE=wavefront or a scene without a persistent instantiation)");
-    const int n_over = overlap_passes();
-    const bool overlap = persistent && !RTW_STRICT_RADIANCE && n_over > 1 && (uint64_t)spp_count >= 2ull * n_over;
-    double* rad[kPassCtrs] = {J.L, nullptr, nullptr};
-    hipEvent_t red_done[kPassCtrs] = {nullptr, nullptr, nullptr};
-    if (overlap) {
-        pass_spp = std::min<uint64_t>(pass_spp, ((uint64_t)spp_count + n_over - 1) / n_over);
-        for (int b = 0; b < 2; ++b) {
-            if ((rc = h->radiance_x[b].ensure(pass_spp * npix * 24))) return rc;
-            rad[b + 1] = static_cast<double*>(h->radiance_x[b].p);
-        }
-        for (hipStream_t* x : {&h->pstream[0], &h->pstream[1], &h->rstream})
-            if (!*x && hipStreamCreateWithFlags(x, hipStreamNonBlocking) != hipSuccess)
-                return rtw_fail(RTW_ERR_HIP, "hipStreamCreate failed");
-        // the side streams start after this call's set-up on the main stream
-        hipEvent_t e = event_at(h, ev++);
-        if (!e) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
-        HIPCHK(hipEventRecord(e, st));
-        for (hipStream_t x : {h->pstream[0], h->pstream[1], h->rstream}) HIPCHK(hipStreamWaitEvent(x, e, 0));
-    }
-    int pi = 0;  // pass index
-    for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp, ++pi) {
+    for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
         J.total = (uint32_t)(S_pass * npix);
         J.spp_pass = S_pass;
         J.s_begin = R.spp_begin + (int)done;
         const uint32_t n0 = std::min<uint32_t>(pool, J.total);
         if (persistent) {
-            hipStream_t sp = st;  // the pass's stream, counters and record buffer
-            ctrs_t* Cp = C;
-            const int b = overlap ? pi % kPassCtrs : 0;
-            if (overlap) {
-                sp = h->pstream[pi & 1];
-                Cp = C + b;
-                J.L = rad[b];
-                if (red_done[b]) HIPCHK(hipStreamWaitEvent(sp, red_done[b], 0));  // buffer b reduced
-            }
-            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kBlock), 0, sp, A, Cp, 0u);  // reset the queue
+            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kBlock), 0, st, A, C, 0u);  // reset the queue
             size_t e0 = 0, e1 = 0;
             if (timed) {
                 e0 = ev++, e1 = ev++;
                 if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
-                HIPCHK(hipEventRecord(h->events[e0], sp));
+                HIPCHK(hipEventRecord(h->events[e0], st));
             }
             if (fast) {
                 FA.J = J;
-                FA.C = Cp;
-                launch_fast(false, h, sp, FA);
+                launch_fast(false, h, st, FA);
             } else {
-                launch_persist(false, h->features, h->shade_mask, h->cus, sp, h->S, J, Cp, h->scene_base,
+                launch_persist(false, h->features, h->shade_mask, h->cus, st, h->S, J, C, h->scene_base,
                                h->shade_bytes, lst_stack_need(h), h->ysph, !h->movers, h->S.n_lights > 0,
                                h->S.background != RTW_BG_GRADIENT && h->S.render_type != RTW_RENDER_NORMAL, pin);
             }
             HIPCHK(hipGetLastError());
             if (timed) {
-                HIPCHK(hipEventRecord(h->events[e1], sp));
+                HIPCHK(hipEventRecord(h->events[e1], st));
                 isect_ev.push_back({e0, e1});
             }
             stats.launches_intersect++;
             stats.iterations++;
-            hipStream_t sr = st;  // the reduction's stream
-            if (overlap) {
-                hipEvent_t kd = event_at(h, ev++);
-                if (!kd) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
-                HIPCHK(hipEventRecord(kd, sp));
-                sr = h->rstream;
-                HIPCHK(hipStreamWaitEvent(sr, kd, 0));
-            }
 #if RTW_PIXEL_MAJOR
             hipLaunchKernelGGL(k_reduce, dim3(reduce_grid(npix)), dim3(kBlock), 0,
-                               sr, J.L, (uint32_t)npix, S_pass, run);
+                               st, J.L, (uint32_t)npix, S_pass, run);
 #else
             if (fast)
-                hipLaunchKernelGGL(k_reduce<float>, dim3(reduce_grid(npix)), dim3(kBlock), 0, sr,
+                hipLaunchKernelGGL(k_reduce<float>, dim3(reduce_grid(npix)), dim3(kBlock), 0, st,
                                    reinterpret_cast<const float*>(J.L), (uint32_t)npix, S_pass, run);
             else
-                hipLaunchKernelGGL(k_reduce<double>, dim3(reduce_grid(npix)), dim3(kBlock), 0, sr, J.L,
+                hipLaunchKernelGGL(k_reduce<double>, dim3(reduce_grid(npix)), dim3(kBlock), 0, st, J.L,
                                    (uint32_t)npix, S_pass, run);
 #endif
             HIPCHK(hipGetLastError());
-            if (overlap) {
-                red_done[b] = event_at(h, ev++);
-                if (!red_done[b]) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
-                HIPCHK(hipEventRecord(red_done[b], sr));
-            }
             stats.samples += J.total;
             continue;
         }
@@ -3861,13 +3792,6 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         stats.samples += J.total;
     }
 
-    if (overlap)  // the main stream continues after every pass and reduction
-        for (hipStream_t x : {h->pstream[0], h->pstream[1], h->rstream}) {
-            hipEvent_t e = event_at(h, ev++);
-            if (!e) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
-            HIPCHK(hipEventRecord(e, x));
-            HIPCHK(hipStreamWaitEvent(st, e, 0));
-        }
     // accum += run
     double* acc_dev = accum_rgb;
     const size_t img_bytes = (size_t)R.nx * R.ny * 24;
@@ -3880,15 +3804,14 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                        (uint32_t)npix, R.nx, R.row_begin, row_step, acc_dev);
     HIPCHK(hipGetLastError());
     if (!R.accum_on_device) HIPCHK(hipMemcpyAsync(accum_rgb, acc_dev, img_bytes, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(&h->host_ctrs[64 - kPassCtrs], C, kPassCtrs * sizeof(ctrs_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&h->host_ctrs[63], C, sizeof(ctrs_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(ev_end, st));
     HIPCHK(hipStreamSynchronize(st));
 
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, ev_begin, ev_end));
     stats.ms_total = ms;
-    for (int b = 64 - kPassCtrs; b < 64; ++b)  // every pass's counters (zeroed at the start)
-        for (int k = 0; k < 8; ++k) stats.segments += h->host_ctrs[b].segments[k].v;
+    for (int k = 0; k < 8; ++k) stats.segments += h->host_ctrs[63].segments[k].v;
     for (auto& p : isect_ev) {
         HIPCHK(hipEventElapsedTime(&ms, h->events[p.first], h->events[p.second]));
         stats.ms_intersect += ms;
