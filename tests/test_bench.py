@@ -214,3 +214,18 @@ def test_bench_line_drops_an_unbounded_valu_figure(bench):
     assert "valu" not in got and "not a roofline fraction" in got["warning"] and got["frac"] == 0.2
     ok = {"frac": 0.2, "valu": {"class_weighted": {"frac": 0.7}}}
     assert bench.bounded_valu(dict(ok)) == ok
+
+
+def test_shared_gpu_rehearsal_is_named_in_the_line(bench, monkeypatch):
+    """RTW_BENCH_SHARED_GPU=1 (every rank on cuda:0, gloo collectives: the
+    one-GPU rehearsal of the N > 1 path, tests/test_gpu_multirank.py) must
+    never pass for an RCCL line: config.parallelism says which it was."""
+    a = parse(bench, monkeypatch, "--gpus", "2")
+    phases = bench.rank_phases({}, 1)
+    samples = a.nx * a.ny * a.spp * a.steps
+    line = bench.result_line(a, 2, a.spp, 1.0, samples, 0, 0.0, None, phases)
+    assert line["config"]["parallelism"] == "spp-shard x2 + RCCL reduce"
+    a.shared_gpu = True
+    line = bench.result_line(a, 2, a.spp, 1.0, samples, 0, 0.0, None, phases)
+    assert "gloo" in line["config"]["parallelism"] and "rehearsal" in line["config"]["parallelism"]
+    assert "RCCL" not in line["config"]["parallelism"]
