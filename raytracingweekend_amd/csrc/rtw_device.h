@@ -250,7 +250,16 @@ RTW_D double canon_raw(uint32_t r1, uint32_t r2) {
 #endif
     // sum in [0, 2^62]: one Markstein step (rtw_div.h div_canon); 0: div_rcp's two
     double r = RTW_CANON_ONESTEP ? div_canon(sum) : div_rcp(sum, kCanonDiv, kCanonRcp);
-    return r >= 1.0 ? kOneMinusUlp : r;
+    // RTW_CANON_MIN: libstdc++'s clamp (r >= 1 ? nextafter(1, 0) : r) as one
+    // v_min_f64 (r is never NaN: sum in [0, 2^62], a finite positive divisor;
+    // every r < 1 is <= nextafter(1, 0)) instead of a compare and two selects.
+    // Measured (1 MI355X, A/B, profiles/r05/ab_r5n_canon_min.log): T 4 740 vs
+    // 4 749 (its constant holds an SGPR pair through the loop), C2 / C3 / C5
+    // +-0.1 %.  Off.
+#ifndef RTW_CANON_MIN
+#define RTW_CANON_MIN 0
+#endif
+    return RTW_CANON_MIN ? __builtin_fmin(r, kOneMinusUlp) : (r >= 1.0 ? kOneMinusUlp : r);
 }
 RTW_D double canon(uint32_t& s) {
     const uint32_t r1 = mr_next(s);

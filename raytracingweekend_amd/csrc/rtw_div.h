@@ -25,6 +25,7 @@
 #define RTW_HD __host__ __device__ __forceinline__
 #else
 #include <cmath>
+#include <cstdint>
 #define RTW_HD inline
 #endif
 
@@ -64,6 +65,29 @@ RTW_HD bool div_rcp_ok_b(double b) {
 RTW_HD bool div_rcp_ok_a(double a) {
     const double m = __builtin_fabs(a);
     return a == 0.0 || (m >= 0x1p-500 && m <= 0x1p500);
+}
+
+// Unsigned 32-bit division by a divisor fixed for a launch (the sample id
+// -> pixel, row decomposition): Granlund-Montgomery's round-up method.  With
+// l = ceil(log2 d) and m = floor(2^32 (2^l - d) / d) + 1 (< 2^32),
+//   t = mulhi(m, n),  n / d = (t + ((n - t) >> s1)) >> s2,  s1 = min(l, 1), s2 = max(l - 1, 0)
+// for every n, d in [1, 2^32) -- one multiply-high, a subtract, an add and two
+// shifts where the compiler's n / d with a run-time d expands to ~18
+// instructions (float reciprocal and two corrections).
+// tests/cpp/udiv_check.cpp: exhaustive over n near every multiple of the
+// image sizes' divisors and random 32-bit operands.
+struct udiv32 {
+    uint32_t m, s1, s2;
+};
+inline udiv32 udiv_magic(uint32_t d) {  // host, d >= 1
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) ++l;
+    const uint64_t m = (((1ull << 32) * ((1ull << l) - d)) / d) + 1;
+    return udiv32{(uint32_t)m, l ? 1u : 0u, l ? l - 1u : 0u};
+}
+RTW_HD uint32_t udiv_fast(uint32_t n, const udiv32& D) {
+    const uint32_t t = (uint32_t)(((uint64_t)D.m * n) >> 32);
+    return (t + ((n - t) >> D.s1)) >> D.s2;
 }
 
 #if defined(__HIPCC__)

@@ -103,6 +103,7 @@ struct job_t {
     uint32_t npix;       // pixels of this call (n_rows * nx)
     int32_t nx, ny, row_begin, row_step, s_begin, max_depth;
     uint32_t spp_pass;   // samples per pixel in this pass
+    rtwd::udiv32 div_npix, div_nx, div_spp;  // magic numbers of npix, nx, spp_pass (sample_coords)
     double* L;           // per-sample radiance, L[3q + c] (pass-local sample id q)
 #if RTW_STRICT_RADIANCE
     // per-thread factor logs of the strict build: bounce k of the path on
@@ -149,14 +150,15 @@ __device__ __forceinline__ void store_record(T* o, T x, T y, T z) {
 
 // pass-local sample id -> pixel (i, j) and global sample index s
 __device__ __forceinline__ void sample_coords(const job_t& J, uint32_t q, int& i, int& j, int& s) {
+// (the quotients by exact magic-number division, rtw_div.h udiv_fast)
 #if RTW_PIXEL_MAJOR
-    const uint32_t rem = q / J.spp_pass;
+    const uint32_t rem = udiv_fast(q, J.div_spp);
     const uint32_t sl = q - rem * J.spp_pass;
 #else
-    const uint32_t sl = q / J.npix;
+    const uint32_t sl = udiv_fast(q, J.div_npix);
     const uint32_t rem = q - sl * J.npix;
 #endif
-    const uint32_t k = rem / (uint32_t)J.nx;
+    const uint32_t k = udiv_fast(rem, J.div_nx);
     i = (int)(rem - k * (uint32_t)J.nx);
     j = J.row_begin + (int)k * J.row_step;
     s = J.s_begin + (int)sl;
@@ -168,13 +170,24 @@ __device__ __forceinline__ ray camera_sample(const job_t& J, uint32_t q, uint32_
     int i, j, s;
     sample_coords(J, q, i, j, s);
     rng = path_seed(J.seed_mix, (uint32_t)(j * J.nx + i), (uint32_t)s);
-    const double u = (double)(i + rnd01(rng)) / (double)J.nx;
-    const double v = (double)(j + rnd01(rng)) / (double)J.ny;
     // The camera (23 doubles) is loaded here, with scalar loads, each time
     // rays are made: an opaque pointer stops the compiler from hoisting it
     // into loop-carried SGPRs of the persistent loop, where it spills.
     const rtw_camera_desc* cp = J.cam;
     asm volatile("" : "+s"(cp));
+    // u = (i + U) / nx, v = (j + U) / ny with the device's own reciprocals of
+    // nx, ny (k_recips, stored after the camera): rtw_div.h's div_hw is the
+    // compiler's division sequence bit for bit when the divisor is in
+    // [2^-200, 2^200] and the numerator 0 or in [2^-800, 2^100] -- here the
+    // divisor is an image size and the numerator 0 or at least 2^-62 (a
+    // canonical draw's grain) and below 2^32; +0 / n gives +0 either way.
+    // With the magic-number sample decomposition, measured (1 MI355X, A/B,
+    // profiles/r05/ab_r5m_udiv_recips.log; bit-identical images,
+    // parity_r5m.log): T 4 741 vs 4 705 (+0.8 %), C3 +1.2 %, C5 -0.5 %,
+    // T fp32 -0.3 %.
+    const double* yr = reinterpret_cast<const double*>(cp + 1);
+    const double u = div_hw((double)(i + rnd01(rng)), (double)J.nx, ld(yr));
+    const double v = div_hw((double)(j + rnd01(rng)), (double)J.ny, ld(yr + 1));
     rtw_camera_desc c;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -232,6 +245,12 @@ __global__ __launch_bounds__(kBlock) void k_fill(paths_t P, ctrs_t* C, uint32_t 
     if (i < n0) P.depth[i] = 0;
     if (i == 0) C->n = n0;
     if (i < kQShards) C->qshard[i].v = 0;
+}
+
+// rcp_hw of the image's width and height for camera_sample, once per render
+// call, into the two doubles after the camera's device copy
+__global__ void k_recips(double* out, int nx, int ny) {
+    if (threadIdx.x == 0) out[0] = rcp_hw((double)nx), out[1] = rcp_hw((double)ny);
 }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() {
@@ -1186,6 +1205,38 @@ enum { K_LAMBL = K_N + 1 };  // (never produced)
 #endif
 constexpr int kSortBlock = RTW_SORT_BLOCK;  // paths regrouped together (one workgroup)
 constexpr int kSortWaves = kSortBlock / 64;
+// DPP (RTW_SORT_DPP): the counting sort's block prefix from a key-major
+// count table s_kc[key][wave] (kKeySlots x 4; slots of keys the scene cannot
+// produce stay zero): lane k < 8 of every wave reads key k's four per-wave
+// counts in one 16-B LDS read and forms their total and the count in the
+// waves before its own; an exclusive scan of the totals over lanes 0..7
+// (three DPP row shifts) adds the paths of every key before k; each lane
+// fetches its own key's base with one ds_bpermute.  The plain form has every
+// lane read all 4 x K_N counts and sum them under selects (~67 VALU per
+// wave-iteration on T).  The same destinations either way (bit-identical
+// images, profiles/r05/parity_r5l.log).  Measured (1 MI355X, A/B,
+// profiles/r05/ab_r5l_sort_dpp.log): T 4 709 vs 4 571 Msamples/s (+3.0 %),
+// T fp32 8 094 vs 7 724 (+4.8 %), C2 +1.0 %, C2 fp32 +0.9 %.
+#ifndef RTW_SORT_DPP
+#define RTW_SORT_DPP 1
+#endif
+constexpr int kKeySlots = 8;
+__device__ __forceinline__ uint32_t sort_base_dpp(const uint32_t (*s_kc)[4], uint32_t lane, uint32_t wave, int key,
+                                                  int k_idle, uint32_t& idle_total) {
+    const uint4 c = *reinterpret_cast<const uint4*>(s_kc[lane & (kKeySlots - 1)]);
+    const uint32_t tot = c.x + c.y + c.z + c.w;
+    const uint32_t before = (wave > 0 ? c.x : 0u) + (wave > 1 ? c.y : 0u) + (wave > 2 ? c.z : 0u);
+    uint32_t incl = tot;  // inclusive scan over lanes 0..7 (row_shr:1, 2, 4; lanes without a source add 0)
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xF, 0xF, true);
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xF, 0xF, true);
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xF, 0xF, true);
+    const uint32_t base = incl - tot + before;
+    idle_total = (uint32_t)__builtin_amdgcn_readlane((int)tot, k_idle);
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(key << 2, (int)base);
+}
+#if RTW_SORT_DPP
+static_assert(kSortWaves == 4 && K_N <= kKeySlots, "RTW_SORT_DPP: 256-thread sort blocks, at most 8 keys");
+#endif
 // HOME_RAY (RTW_SORT_HOME_RAY): a path's ray and sample id live in its home
 // slot beside its throughput, so the exchange moves only the record's home
 // index, hit (t, prim), engine and depth -- 5 values instead of 12 -- and the
@@ -1197,7 +1248,12 @@ template <int F, int M, bool LDS>
 __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist_sort(persist_args) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
+#if RTW_SORT_DPP
+    __shared__ __attribute__((aligned(16))) uint32_t s_kc[kKeySlots][kSortWaves];  // per key, lanes per wave
+    if (threadIdx.x < kKeySlots * kSortWaves) (&s_kc[0][0])[threadIdx.x] = 0u;  // (before the barrier below)
+#else
     __shared__ uint32_t s_kc[kSortWaves][K_N];  // per wave, lanes per key
+#endif
     __shared__ uint32_t s_seg[kSortWaves];
     constexpr bool HR = RTW_SORT_HOME_RAY != 0;
     constexpr int kX = HR ? 1 : kSortBlock;  // exchange arrays HOME_RAY does without
@@ -1354,9 +1410,17 @@ void k_persist_sort(persist_args) {
             if (!key_used(k)) continue;
             const unsigned long long m = __ballot(key == k);
             if (key == k) rank_in_wave = (uint32_t)__popcll(m & lanemask_lt());
+#if RTW_SORT_DPP
+            if (lane == 0) s_kc[k][wave] = (uint32_t)__popcll(m);
+#else
             if (lane == 0) s_kc[wave][k] = (uint32_t)__popcll(m);
+#endif
         }
         __syncthreads();
+#if RTW_SORT_DPP
+        uint32_t idle_total;
+        const uint32_t dst = rank_in_wave + sort_base_dpp(s_kc, lane, wave, key, K_IDLE, idle_total);
+#else
         uint32_t dst = rank_in_wave, idle_total = 0;
 #pragma unroll
         for (int k = 0; k < K_N; ++k) {
@@ -1372,6 +1436,7 @@ void k_persist_sort(persist_args) {
             if (k == key) dst += before;
             if (k == K_IDLE) idle_total = tot;
         }
+#endif
         if (idle_total == kSortBlock) break;  // block-uniform: nothing left to trace or take
         pk.mark(PS_HIT);
         // 4. move every path to the slot of its rank (an idle record's ray
@@ -1674,7 +1739,13 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
     using namespace rtwf;
     constexpr bool NOISE = (F & FF_NONOISE) == 0;
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
+#if RTW_SORT_DPP
+    static_assert(FK_N <= kKeySlots, "RTW_SORT_DPP: at most 8 keys");
+    __shared__ __attribute__((aligned(16))) uint32_t s_kc[kKeySlots][kSortWaves];  // per key, lanes per wave
+    if (threadIdx.x < kKeySlots * kSortWaves) (&s_kc[0][0])[threadIdx.x] = 0u;  // (before the barrier below)
+#else
     __shared__ uint32_t s_kc[kSortWaves][FK_N];
+#endif
     __shared__ uint32_t s_seg[kSortWaves];
     __shared__ float x_o[3][kSortBlock], x_d[3][kSortBlock], x_tm[kSortBlock], x_t[kSortBlock];
     __shared__ int32_t x_prim[kSortBlock];
@@ -1758,9 +1829,17 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
         for (int k = 0; k < FK_N; ++k) {
             const unsigned long long m = __ballot(key == k);
             if (key == k) rank_in_wave = (uint32_t)__popcll(m & lanemask_lt());
+#if RTW_SORT_DPP
+            if (lane == 0) s_kc[k][wave] = (uint32_t)__popcll(m);
+#else
             if (lane == 0) s_kc[wave][k] = (uint32_t)__popcll(m);
+#endif
         }
         __syncthreads();
+#if RTW_SORT_DPP
+        uint32_t idle_total;
+        const uint32_t dst = rank_in_wave + sort_base_dpp(s_kc, lane, wave, key, FK_IDLE, idle_total);
+#else
         uint32_t dst = rank_in_wave, idle_total = 0;
 #pragma unroll
         for (int k = 0; k < FK_N; ++k) {
@@ -1775,6 +1854,7 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
             if (k == key) dst += before;
             if (k == FK_IDLE) idle_total = tot;
         }
+#endif
         if (idle_total == kSortBlock) break;  // block-uniform: nothing left to trace or take
         // 4. move every path to the slot of its rank
         if (depth != 0) {
@@ -3597,12 +3677,17 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
 
     job_t J;
     h->cam_host = *camera;
-    if ((rc = h->camera.ensure(sizeof(rtw_camera_desc)))) return rc;
+    if ((rc = h->camera.ensure(sizeof(rtw_camera_desc) + 2 * sizeof(double)))) return rc;
     HIPCHK(hipMemcpyAsync(h->camera.p, &h->cam_host, sizeof(rtw_camera_desc), hipMemcpyHostToDevice, st));
     J.cam = static_cast<const rtw_camera_desc*>(h->camera.p);
+    hipLaunchKernelGGL(k_recips, dim3(1), dim3(64), 0, st,
+                       reinterpret_cast<double*>(static_cast<char*>(h->camera.p) + sizeof(rtw_camera_desc)), R.nx, R.ny);
+    HIPCHK(hipGetLastError());
     J.seed_mix = host_splitmix64(R.seed);
     J.npix = (uint32_t)npix;
     J.nx = R.nx, J.ny = R.ny, J.row_begin = R.row_begin, J.row_step = row_step;
+    J.div_npix = rtwd::udiv_magic(J.npix);
+    J.div_nx = rtwd::udiv_magic((uint32_t)R.nx);
     J.max_depth = R.max_depth;
     J.L = static_cast<double*>(h->radiance.p);
 #if RTW_STRICT_RADIANCE
@@ -3667,6 +3752,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
         J.total = (uint32_t)(S_pass * npix);
         J.spp_pass = S_pass;
+        J.div_spp = rtwd::udiv_magic(S_pass);
         J.s_begin = R.spp_begin + (int)done;
         const uint32_t n0 = std::min<uint32_t>(pool, J.total);
         if (persistent) {
