@@ -90,6 +90,18 @@ RTW_HD uint32_t udiv_fast(uint32_t n, const udiv32& D) {
     return (t + ((n - t) >> D.s1)) >> D.s2;
 }
 
+// x mod (2^31 - 2) for a 64-bit x (the per-sample seed, rtw_path_seed): as
+// 2^31 = 2 (mod 2^31 - 2), x = a 2^31 + b folds to 2a + b < 2^35, which folds
+// once more below 2^31 + 18, and one conditional subtract ends it -- 32-bit
+// shifts, masks and adds where a 64-bit remainder by a constant costs a
+// 64 x 64 multiply-high (tests/cpp/udiv_check.cpp: equal to x % m).
+RTW_HD uint32_t mod_2p31m2(uint64_t x) {
+    constexpr uint32_t m = 2147483646u;
+    const uint64_t y = ((x >> 31) << 1) + (x & 0x7fffffffu);
+    const uint32_t z = (uint32_t)((y >> 31) << 1) + (uint32_t)(y & 0x7fffffffu);
+    return z >= m ? z - m : z;
+}
+
 #if defined(__HIPCC__)
 // Shared-divisor quotients, bit for bit the compiler's own a / b.
 //

@@ -49,6 +49,23 @@ int main(int argc, char** argv) {
             }
         for (long k = 0; k < per; ++k) check((uint32_t)next(), d, D);
     }
+    // the seed fold: x mod (2^31 - 2) for 64-bit x
+    const unsigned long long M = 2147483646ull;
+    uint64_t mcases = 0, mbad = 0;
+    auto mcheck = [&](uint64_t x) {
+        ++mcases;
+        if (rtwd::mod_2p31m2(x) != x % M && mbad++ < 10)
+            std::printf("mod mismatch x=%llu\n", (unsigned long long)x);
+    };
+    for (uint64_t x : {0ull, 1ull, M - 1, M, M + 1, 2 * M, ~0ull, ~0ull - 1, (1ull << 31) - 1, 1ull << 31,
+                       (1ull << 32) - 1, 1ull << 32, (1ull << 35) - 1})
+        mcheck(x);
+    for (uint64_t k = 1; k < (1ull << 33); k += 1 + (next() & 0xfffff))  // next to multiples of M
+        for (int64_t o = -3; o <= 3; ++o) mcheck(k * M + (uint64_t)o);
+    for (long k = 0; k < 100 * per; ++k) mcheck(next());
+    for (long k = 0; k < 100 * per; ++k) mcheck(next() >> (next() % 64));
+    bad += mbad;
+    std::printf("mod cases %llu mismatches %llu\n", (unsigned long long)mcases, (unsigned long long)mbad);
     std::printf("udiv cases %llu mismatches %llu\n", (unsigned long long)cases, (unsigned long long)bad);
     return bad ? 1 : 0;
 }

@@ -24,10 +24,11 @@ def test_magic_number_division_is_exact(tmp_path):
     every camera sample) equals n / d on 32-bit operands: every divisor up to
     4 096, the image widths and pixel counts, powers of two and their
     neighbours, random divisors; n next to each multiple, at the range ends
-    and random (tests/cpp/udiv_check.cpp)."""
+    and random (tests/cpp/udiv_check.cpp); and mod_2p31m2 (the per-sample seed
+    fold) equals x % (2^31 - 2) on 64-bit x."""
     exe = tmp_path / "udiv_check"
     subprocess.run(["g++", "-std=c++17", "-O2", f"-I{ROOT / 'raytracingweekend_amd' / 'csrc'}",
                     str(ROOT / "tests" / "cpp" / "udiv_check.cpp"), "-o", str(exe)], check=True)
     r = subprocess.run([str(exe), "2000"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "mismatches 0" in r.stdout and "udiv cases 0 " not in r.stdout
+    assert r.stdout.count("mismatches 0") == 2 and "udiv cases 0 " not in r.stdout
