@@ -1,6 +1,12 @@
 """Static VALU cost of one kernel by source line (hipcc -S -g1 ISA).
 
-  python scripts/isa_lines.py KS.s FUNCTION-SUBSTRING [TOP]
+  python scripts/isa_lines.py KS.s FUNCTION-SUBSTRING [TOP] [--outer FILE]
+
+--outer FILE charges each instruction to the OUTERMOST line of FILE in its
+inline chain (e.g. --outer rtw_kernels.hip: which call site of the kernel
+body the instruction belongs to -- camera sample, world walk, sort prefix,
+shading) instead of the innermost line.  That view found the counting
+sort's block prefix (~67 VALU per wave-iteration).
 
 Each v_* instruction is weighted by its measured issue cost on gfx950
 (scripts/valu_rates.hip, profiles/r01/valu_rates.log: fp64 ~4.7 cycles per wave
@@ -12,8 +18,14 @@ import re
 import sys
 from collections import defaultdict
 
-path, fname = sys.argv[1], sys.argv[2]
-top = int(sys.argv[3]) if len(sys.argv) > 3 else 40
+args = sys.argv[1:]
+outer = None
+if "--outer" in args:
+    k = args.index("--outer")
+    outer = args[k + 1]
+    del args[k:k + 2]
+path, fname = args[0], args[1]
+top = int(args[2]) if len(args) > 2 else 40
 lines = open(path).read().splitlines()
 files = {}
 for l in lines:
@@ -42,6 +54,9 @@ for l in lines[start:end]:
     m = re.match(r"\.loc\s+(\d+)\s+(\d+)", s)
     if m:
         cur = f"{files.get(m.group(1), m.group(1))}:{m.group(2)}"
+        if outer:  # the outermost frame of `outer` in the comment's inline chain
+            frames = re.findall(re.escape(outer) + r":(\d+)", l)
+            cur = f"{outer}:{frames[-1]}" if frames else "(other)"
         continue
     m = re.match(r"(v_\w+)", s)
     if m:
