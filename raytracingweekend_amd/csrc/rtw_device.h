@@ -375,11 +375,33 @@ RTW_D d3 random_cosine_direction(uint32_t& s) {  // utility.h:54-67
 struct onb {
     d3 u, v, w;
 };
+// RTW_SQRT_UNIT: vectors whose length is known to be about 1 are normalised
+// with rtw_div.h's bare sqrt sequence (sqrt_core: the compiler's sqrt for x
+// >= 2^-766, without its range and class handling -- no branch, no vote):
+// the second axis of every frame (cross(w, a) with w unit and |w.x| <= 0.9
+// when a = x, so |.|^2 >= 0.19 -- or >= 0.81), and frame_w of a lambertian
+// surface's normal (hit_record: (p - c) / r of a sphere, an axis normal,
+// rotated orthogonally; surf_frame::unit, a constant where shade_core builds
+// the frame -- a per-lane choice of the two forms made the frame a scratch
+// object).  A non-finite vector gives NaN either way.  0: the compiler's
+// sqrt (A/B).  Measured (1 MI355X, A/B, profiles/r05/ab_r5r_sqrt_unit.log;
+// bit-identical images, parity_r5r.log): T 4 762 vs 4 752, C3 +0.25 %, C2
+// and C5 +-0.
+#ifndef RTW_SQRT_UNIT
+#define RTW_SQRT_UNIT 1
+#endif
+RTW_HD d3 normalize_unit(d3 v) {
+#if defined(__HIP_DEVICE_COMPILE__) && RTW_SQRT_CORE && RTW_SQRT_UNIT
+    return v / sqrt_core(len2(v));
+#else
+    return normalize_b(v);
+#endif
+}
 RTW_HD onb onb_from_w(d3 n) {  // onb.h:32-38
     onb b;
     b.w = normalize_b(n);
     const d3 a = (fabs(b.w.x) > 0.9) ? d3{0, 1, 0} : d3{1, 0, 0};
-    b.v = normalize_b(cross(b.w, a));
+    b.v = normalize_unit(cross(b.w, a));
     b.u = cross(b.w, b.v);
     return b;
 }
@@ -2519,6 +2541,7 @@ struct surf_frame {
     d3 n;
     int32_t prim;
     bool rect;
+    bool unit;  // n is a surface normal (length about 1: normalize_unit)
 };
 RTW_D onb frame_onb(const scene& S, const surf_frame& s) {
     if (s.rect) {
@@ -2528,7 +2551,7 @@ RTW_D onb frame_onb(const scene& S, const surf_frame& s) {
     return onb_from_w(s.n);
 }
 RTW_D d3 frame_w(const scene& S, const surf_frame& s) {  // == frame_onb(S, s).w
-    return s.rect ? ld3(S.prim_onb + 9 * (size_t)s.prim + 6) : normalize(s.n);
+    return s.rect ? ld3(S.prim_onb + 9 * (size_t)s.prim + 6) : (s.unit ? normalize_unit(s.n) : normalize(s.n));
 }
 
 // mixture_pdf(cosine_pdf(n), hittable_pdf(lights, o))::generate (pdf.h:55-79)
@@ -2563,6 +2586,7 @@ RTW_D d3 mixture_generate(const scene& S, const surf_frame& sf, d3 o, uint32_t& 
         const double distance_squared = len2(direction);
         bf.n = direction;
         bf.rect = false;
+        bf.unit = false;
         a1 = 1 - q.p[9] / distance_squared;  // radius * radius / distance_squared
     }
     const double s1 = RTW_SQRT(a1);

@@ -528,7 +528,7 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
         // decision reads -- directions, t, the sign of pdf_val -- is the
         // reference's own arithmetic.  See RTW_RADIANCE_FAST below.)
         // onb::build_from_w(normal) (onb.h:32-38), built where it is used
-        const surf_frame sf{n, prim, rect};
+        const surf_frame sf{n, prim, rect, true};
         pf.mark(PS_HIT);
         d3 dir;
         double pdf_val, cosine;
