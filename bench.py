@@ -235,6 +235,10 @@ def roofline(args, kernel, build, seg, ms, launches, algo, check=True):
     if rec.get("write_bytes_per_launch") is not None:
         out["write_bytes"] = round(rec["write_bytes_per_launch"] * scale, 1)
     secs = avg_ms * 1e-3
+    if rec.get("clock_ghz_x_ms") and rec.get("avg_launch_ms"):
+        # the clock the record's launches ran at (GRBM busy cycles / launch time): the peaks
+        # below assume 2.4 GHz; a power-limited box runs some workloads slower
+        out["pmc_clock_ghz"] = round(rec["clock_ghz_x_ms"] / rec["avg_launch_ms"], 3)
     v = {"valu_insts_per_wave_segment": round(rec["valu_insts_per_wave_segment"], 1),
          "lane_util": round(rec["valu_lane_util"], 4) if rec.get("valu_lane_util") else None}
     cyc = rec.get("valu_class_cycles_per_segment")

@@ -77,6 +77,11 @@ def test_pmc_record_must_match_kernel_build_and_workload(bench, monkeypatch, tmp
     assert abs(fl["issued"] - 400.0 * 1e9 / 0.05 / 1e12) < 1e-9 and fl["peak"] == 78.6
     assert abs(fl["achieved"] - 0.5 * 400.0 * 1e9 / 0.05 / 1e12) < 1e-9
     assert r3["write_bytes"] == 5e8
+    assert "pmc_clock_ghz" not in r3  # the record carries no clock
+    rec5 = dict(rec2, clock_ghz_x_ms=237.0, avg_launch_ms=100.0)  # GRBM cycles: 2.37 GHz
+    (tmp_path / "T.json").write_text(json.dumps(rec5))
+    r5 = bench.roofline(a, rec["kernel"], "abc", seg=2e9, ms=100.0, launches=2, algo=68 * 2e9)
+    assert r5["pmc_clock_ghz"] == 2.37
     r2 = bench.roofline(a, rec["kernel"], "stale", seg=2e9, ms=100.0, launches=2, algo=68 * 2e9)
     assert r2["bound"] == "hbm" and r2["traffic"] is None and "no PMC record" in r2["pmc"] and "valu" not in r2
     # a fraction above 1 is refused, never reported
