@@ -1524,6 +1524,10 @@ struct fast_args {
     ctrs_t* C;
     rtwf::cam32 cam;
     uint32_t lds_nodes;  // k_fast<.., LST>: BVH node packet (the top nodes) in dynamic LDS
+    // k_fast_sort<.., LDS>: each fscene array's byte offset in the LDS copy of
+    // the shading prefix, ~0u for one outside it (host-computed: lds_fscene's
+    // two 64-bit range compares per pointer per use become one 32-bit test)
+    uint32_t lds_off[9];
 };
 
 // fast_args re-read from the kernarg segment by each phase that uses it
@@ -1703,6 +1707,32 @@ void k_fast(fast_args) {
     }
 }
 
+// RTW_FAST_LDS_OFF: k_fast_sort re-points its scene with the host's offsets
+// (fast_args::lds_off) instead of range-testing every pointer at every use --
+// two 64-bit compares, a subtract and selects per pointer, twice per
+// iteration, on the scalar unit, which the fp32 kernel's issue shares with
+// ~840 VALU per wave-segment (~680 SALU).  Measured (1 MI355X, A/B,
+// profiles/r05/ab_r5t_fast_lds_off.log; bit-identical, parity_r5t.log):
+// T fp32 8 654 vs 8 075 Msamples/s (+7.2 %), T fp64 +-0.  (The same offsets
+// for k_persist_sort's lds_scene, whose rebase has no range test, added
+// SALU and VALU there: not used.)
+#ifndef RTW_FAST_LDS_OFF
+#define RTW_FAST_LDS_OFF 1
+#endif
+__device__ __forceinline__ rtwf::fscene lds_fscene_off(const rtwf::fscene& S, const uint32_t* off, const char* lds) {
+    rtwf::fscene L = S;
+    auto rb = [&](const void* p, uint32_t o) -> const void* { return o != ~0u ? (const void*)(lds + o) : p; };
+    L.prims = (const rtwf::prim32*)rb(S.prims, off[0]);
+    L.entries = (const rtwf::ent32*)rb(S.entries, off[1]);
+    L.ops = (const rtwf::op32*)rb(S.ops, off[2]);
+    L.materials = (const rtwf::mat32*)rb(S.materials, off[3]);
+    L.textures = (const rtwf::tex32*)rb(S.textures, off[4]);
+    L.lights = (const rtw_light*)rb(S.lights, off[5]);
+    L.ranvec = (const float*)rb(S.ranvec, off[6]);
+    L.perm = (const int32_t*)rb(S.perm, off[7]);
+    L.frames = (const float*)rb(S.frames, off[8]);
+    return L;
+}
 // Re-point an fp32 scene's arrays into an LDS copy of its allocation.
 __device__ __forceinline__ rtwf::fscene lds_fscene(const rtwf::fscene& S, const char* base, uint32_t bytes,
                                                    const char* lds) {
@@ -1820,7 +1850,11 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
             h = world_closest<F>(fast_args_now().S, r, rng, stk);
             ++segs;
             const fast_args& A = fast_args_now();
+#if RTW_FAST_LDS_OFF
+            key = hit_key(LDS ? lds_fscene_off(A.S, A.lds_off, s_scene) : A.S, h);
+#else
             key = hit_key(LDS ? lds_fscene(A.S, base, bytes, s_scene) : A.S, h);
+#endif
         }
         // 3. counting sort of the block's paths by key
         const uint32_t my_home = x_home[me], my_q = x_q[me];
@@ -1876,7 +1910,11 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
             const fray rr{f3{x_o[0][me], x_o[1][me], x_o[2][me]}, f3{x_d[0][me], x_d[1][me], x_d[2][me]}, x_tm[me]};
             const fhit hh{x_t[me], x_prim[me], false};
             const fast_args& A = fast_args_now();
+#if RTW_FAST_LDS_OFF
+            const seg_f sg = shade<NOISE>(LDS ? lds_fscene_off(A.S, A.lds_off, s_scene) : A.S, rr, hh, rng, depth);
+#else
             const seg_f sg = shade<NOISE>(LDS ? lds_fscene(A.S, base, bytes, s_scene) : A.S, rr, hh, rng, depth);
+#endif
             const uint32_t home = x_home[me];
             const f3 thr{s_thr[0][home], s_thr[1][home], s_thr[2][home]};
             if (sg.cont) {
@@ -3289,7 +3327,14 @@ void launch_fast_sort_t(bool probe, std::string* name, int cus, hipStream_t st, 
     if (probe) return;
     const size_t shm = LL ? bytes : 0;
     const int grid = grid_blocks(reinterpret_cast<const void*>(&k_fast_sort<FF, LL>), kSortBlock, shm, cus);
-    hipLaunchKernelGGL((k_fast_sort<FF, LL>), dim3(grid), dim3(kSortBlock), shm, st, A, base, bytes);
+    fast_args a = A;  // the arrays' offsets in the LDS copy (lds_fscene_off)
+    const void* ptrs[9] = {A.S.prims, A.S.entries, A.S.ops, A.S.materials, A.S.textures,
+                           A.S.lights, A.S.ranvec, A.S.perm, A.S.frames};
+    for (int k = 0; k < 9; ++k) {
+        const char* c = static_cast<const char*>(ptrs[k]);
+        a.lds_off[k] = (c && base && c >= base && c < base + bytes) ? (uint32_t)(c - base) : ~0u;
+    }
+    hipLaunchKernelGGL((k_fast_sort<FF, LL>), dim3(grid), dim3(kSortBlock), shm, st, a, base, bytes);
 }
 // RTW_FAST_SORT=0: list scenes take k_fast too (A/B)
 bool fast_sort_enabled() {

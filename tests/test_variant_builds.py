@@ -40,6 +40,7 @@ VARIANTS = {
     "canon_min": T + ["-DRTW_CANON_MIN=1"],
     "seed_fold": T + ["-DRTW_SEED_FOLD=1"],
     "sqrt_unit_off": C3 + ["-DRTW_SQRT_UNIT=0"],
+    "fast_lds_rangecheck": T + ["-DRTW_FAST_LDS_OFF=0"],
     "profiling": T + ["-DRTW_PROF"],
     "bvh4": C3 + ["-DRTW_BVH4=1"],
     "packet": C3 + ["-DRTW_PACKET=1"],
