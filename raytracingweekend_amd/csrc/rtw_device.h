@@ -791,8 +791,17 @@ RTW_D rect_rcp make_rect_rcp(const scene& S, const ray& r) {
     }
     return q;
 }
-// rect_axis_t with the walk's shared reciprocal of d.K
-template <int K, int A, int B>
+// rect_axis_t with the walk's shared reciprocal of d.K.  BL (the world list
+// walk's rects, RTW_RECT_BRANCHLESS): the same comparisons without the early
+// return -- a and b formed for every lane, one branch level less of
+// exec-mask bookkeeping on the scalar unit per rect.  Measured (1 MI355X,
+// A/B, profiles/r05/ab_r5u_rect_branchless.log; bit-identical images): T
+// 4 811 vs 4 747 (+1.3 %); in the BVH leaves' box faces (mostly missed, the
+// early return skips their a, b) C5 -1.2 %, so those keep it.
+#ifndef RTW_RECT_BRANCHLESS
+#define RTW_RECT_BRANCHLESS 1
+#endif
+template <int K, int A, int B, bool BL = false>
 RTW_D bool rect_axis_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, double t0, double t1,
                          double& t_out) {
     const double ok = K == 0 ? r.o.x : (K == 1 ? r.o.y : r.o.z);
@@ -803,6 +812,13 @@ RTW_D bool rect_axis_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, do
         asm volatile("");  // keeps the exact division behind the branch
         t = num / od;
     }
+    if constexpr (BL) {
+        const double a = (A == 0 ? r.o.x : r.o.y) + t * (A == 0 ? r.d.x : r.d.y);
+        const double b = (B == 1 ? r.o.y : r.o.z) + t * (B == 1 ? r.d.y : r.d.z);
+        const bool hit = !(t < t0 || t > t1) && !(a < q.p[0] || a > q.p[1] || b < q.p[2] || b > q.p[3]);
+        t_out = t;
+        return hit;
+    }
     if (t < t0 || t > t1) return false;
     const double a = (A == 0 ? r.o.x : r.o.y) + t * (A == 0 ? r.d.x : r.d.y);
     const double b = (B == 1 ? r.o.y : r.o.z) + t * (B == 1 ? r.d.y : r.d.z);
@@ -811,9 +827,10 @@ RTW_D bool rect_axis_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, do
     return true;
 }
 RTW_D bool rect_t_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, double t0, double t1, double& t_out) {
-    if (q.type == RTW_PRIM_RECT_XY) return rect_axis_rcp<2, 0, 1>(q, r, rr, t0, t1, t_out);
-    if (q.type == RTW_PRIM_RECT_XZ) return rect_axis_rcp<1, 0, 2>(q, r, rr, t0, t1, t_out);
-    return rect_axis_rcp<0, 1, 2>(q, r, rr, t0, t1, t_out);
+    constexpr bool BL = RTW_RECT_BRANCHLESS != 0;  // (the world list walk's rects)
+    if (q.type == RTW_PRIM_RECT_XY) return rect_axis_rcp<2, 0, 1, BL>(q, r, rr, t0, t1, t_out);
+    if (q.type == RTW_PRIM_RECT_XZ) return rect_axis_rcp<1, 0, 2, BL>(q, r, rr, t0, t1, t_out);
+    return rect_axis_rcp<0, 1, 2, BL>(q, r, rr, t0, t1, t_out);
 }
 
 #ifndef RTW_RECT_RCP

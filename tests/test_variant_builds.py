@@ -41,6 +41,7 @@ VARIANTS = {
     "seed_fold": T + ["-DRTW_SEED_FOLD=1"],
     "sqrt_unit_off": C3 + ["-DRTW_SQRT_UNIT=0"],
     "fast_lds_rangecheck": T + ["-DRTW_FAST_LDS_OFF=0"],
+    "rect_early_return": T + ["-DRTW_RECT_BRANCHLESS=0"],
     "profiling": T + ["-DRTW_PROF"],
     "bvh4": C3 + ["-DRTW_BVH4=1"],
     "packet": C3 + ["-DRTW_PACKET=1"],
