@@ -34,6 +34,7 @@ restatement when that binary is absent).
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import socket
@@ -71,6 +72,10 @@ VALU_COST = {"FMA_F64": 4.59, "MUL_F64": 4.59, "ADD_F64": 4.59, "TRANS_F64": 16.
              "FMA_F32": 2.60, "ADD_F32": 2.60, "MUL_F32": 2.60, "TRANS_F32": 8.36}
 VALU_COST_OTHER = 2.55
 PMC_DIR = ROOT / "profiles" / "pmc"
+# Process-group timeout: a rank stuck in a collective (or a rank that never
+# joins) ends the run with a per-rank error after this many seconds instead of
+# holding the driver's whole time limit.
+PG_TIMEOUT_S = float(os.environ.get("RTW_BENCH_PG_TIMEOUT", "240"))
 
 # BASELINE.json configs; spp is the image's TOTAL samples per pixel
 WORKLOADS = {
@@ -324,7 +329,36 @@ def rank_phases(local: dict, world: int, device=None) -> dict:
             for i, k in enumerate(RANK_PHASES)}
 
 
-def result_line(args, world, spp_total, elapsed, samples, seg, ms_gpu, roof, phases) -> dict:
+def device_record(gpu: int) -> dict:
+    """What this rank runs on: the HIP device index and the card's PCI
+    address (domain:bus:device, as rocm-smi prints it) and name."""
+    import torch
+    p = torch.cuda.get_device_properties(gpu)
+    return {"device": gpu, "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "name": p.name, "arch": getattr(p, "gcnArchName", "")}
+
+
+def rank_devices(world: int, rank: int, local_rank: int, dev_rec: dict) -> dict:
+    """The line's record of who ran where: every rank's {rank, local_rank,
+    device, pci_bus_id, ...} gathered over the process group
+    (all_gather_object), the group's backend and world size, and how many
+    distinct cards the ranks used -- so an N > 1 line shows by itself whether
+    RCCL saw N ranks on N distinct devices."""
+    me = {"rank": rank, "local_rank": local_rank, **dev_rec}
+    if world > 1:
+        import torch.distributed as dist
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+        backend = dist.get_backend()
+        size = dist.get_world_size()
+    else:
+        ranks, backend, size = [me], None, 1
+    ranks = sorted(ranks, key=lambda r: r["rank"])
+    return {"process_group": {"backend": backend, "world_size": size, "timeout_s": PG_TIMEOUT_S if world > 1 else None},
+            "ranks": ranks, "distinct_devices": len({r.get("pci_bus_id") for r in ranks})}
+
+
+def result_line(args, world, spp_total, elapsed, samples, seg, ms_gpu, roof, phases, placement=None) -> dict:
     """The rank-0 JSON line (the driver's contract): value = all samples of
     the timed steps / the step time (max over ranks)."""
     samples_per_step = args.nx * args.ny * spp_total
@@ -350,6 +384,8 @@ def result_line(args, world, spp_total, elapsed, samples, seg, ms_gpu, roof, pha
         # per-rank ms per step, max / min over the ranks and rank 0's own
         # (a slow rank, the RCCL reduce and the finalize in an N > 1 run)
         "rank_phases_ms": phases,
+        # every rank's device and the process group (rank_devices)
+        **(placement or {}),
         "cpu_baseline": None,
     }
 
@@ -380,10 +416,12 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     if world > 1:
+        timeout = datetime.timedelta(seconds=PG_TIMEOUT_S)
         if args.shared_gpu:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=timeout)
+    placement = rank_devices(world, rank, local_rank, device_record(gpu))
 
     nx, ny, depth = args.nx, args.ny, args.depth
     spp_total = args.spp if args.scaling == "strong" else args.spp * world
@@ -440,7 +478,7 @@ def main():
         if roof:
             roof["bvh_lds_nodes"] = info["bvh_lds_nodes"]  # BVH node packet staged in LDS per workgroup
         ms_gpu = sum(s["ms_total"] for s in stats) / max(len(stats), 1)
-        out = result_line(args, world, spp_total, elapsed, samples, seg, ms_gpu, roof, phases)
+        out = result_line(args, world, spp_total, elapsed, samples, seg, ms_gpu, roof, phases, placement)
         if world == 1 and not args.no_cpu_baseline:
             threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
             try:

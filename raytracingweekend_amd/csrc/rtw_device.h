@@ -123,32 +123,9 @@ RTW_HD d3 operator+(d3 a, d3 b) { return d3{a.x + b.x, a.y + b.y, a.z + b.z}; }
 RTW_HD d3 operator-(d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 RTW_HD d3 operator*(d3 a, d3 b) { return d3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 RTW_HD d3 operator*(d3 a, double s) { return d3{a.x * s, a.y * s, a.z * s}; }
-// d3 / double (vec3.h operator/): on the device the three quotients share one
-// reciprocal (rtw_div.h rcp_hw / div_hw, bit for bit the compiler's own a / b
-// when |s| is in [2^-200, 2^200] and each |a| in [2^-800, 2^100]; a zero
-// numerator takes q = a * y, which carries division's sign rule); a wave
-// with a lane outside the range divides exactly.
-// Measured (1 MI355X, A/B, profiles/r04/ab_div3_r4m.log; GPU suite green
-// with it): T 4 293 vs 4 440, C2 -0.7 %, C3 -2.6 %, C5 -2.5 % -- the range
-// checks, the wave vote and two more spilled VGPRs cost more than the two
-// hardware division sequences they replace.  Off.
-#ifndef RTW_DIV3_SHARED
-#define RTW_DIV3_SHARED 0
-#endif
-RTW_HD d3 operator/(d3 a, double s) {
-#if defined(__HIP_DEVICE_COMPILE__) && RTW_DIV3_SHARED
-    const bool ok = div_hw_ok_b_exp(s) && div_hw_ok_a0_exp(a.x) && div_hw_ok_a0_exp(a.y) && div_hw_ok_a0_exp(a.z);
-    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {  // wave-uniform: no divergent branch
-        const double y = rcp_hw(s);
-        auto q = [&](double v) {
-            const double q0 = v * y;
-            return v == 0.0 ? q0 : div_hw(v, s, y);
-        };
-        return d3{q(a.x), q(a.y), q(a.z)};
-    }
-#endif
-    return d3{a.x / s, a.y / s, a.z / s};
-}
+// d3 / double (vec3.h operator/): three IEEE divisions.  (Sharing one
+// reciprocal behind a range vote measured T -3.3 %: DESIGN.md §4.2b.)
+RTW_HD d3 operator/(d3 a, double s) { return d3{a.x / s, a.y / s, a.z / s}; }
 RTW_HD d3 operator-(d3 a) { return d3{-a.x, -a.y, -a.z}; }
 // a / b for a quantity that only scales radiance (RTW_RADIANCE_RCP)
 __device__ __forceinline__ double rad_div(double a, double b) {
@@ -159,22 +136,11 @@ __device__ __forceinline__ double rad_div(double a, double b) {
 }
 RTW_HD double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RTW_HD double len2(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-// RTW_PACKET_ALL: node_at reads the LDS packet without a per-lane
-// address-space test when every node of the scene is in it (a wave-uniform
-// test of the packet size; fp64 and fp32 walks).  Measured (1 MI355X, A/B,
-// profiles/r05/ab_r5c_*.log): C5 slice 691 vs 675 alone, 703 with
-// RTW_RNG_JUMP; C3 3 148 vs 3 058 with it; T ±0.
-#ifndef RTW_PACKET_ALL
-#define RTW_PACKET_ALL 1
-#endif
-// RTW_SQRT_CORE: fp64 square roots as rtw_div.h's sqrt_w (the compiler's own
-// sequence without its range scaling and class fixup, taken when the whole
-// wave is in range; bit for bit the same value) or sqrt_core where the range
-// is known (1 - a canonical draw).  0: the compiler's sqrt everywhere (A/B).
-#ifndef RTW_SQRT_CORE
-#define RTW_SQRT_CORE 1
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && RTW_SQRT_CORE
+// fp64 square roots as rtw_div.h's sqrt_w (the compiler's own sequence
+// without its range scaling and class fixup, taken when the whole wave is in
+// range; bit for bit the same value) or sqrt_core where the range is known
+// (1 - a canonical draw).  Measured T +0.5 %, C5 +1.7 %.
+#if defined(__HIP_DEVICE_COMPILE__)
 #define RTW_SQRT(x) sqrt_w(x)
 #define RTW_SQRT_POS(x) sqrt_core(x)  // x in [2^-766, 2^1024): callers argue it
 #else
@@ -185,18 +151,9 @@ RTW_HD double len(d3 a) { return __builtin_sqrt(len2(a)); }
 RTW_HD d3 cross(d3 a, d3 b) {  // vec3.h:54-59
     return d3{a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x};
 }
-// RTW_SQRT_NORM: normalize's length through sqrt_w too.  Measured (1 MI355X,
-// A/B, profiles/r05/ab_r5b_*.log): T 4 465 vs 4 523 without it, C5 slice 663
-// vs 676, C3 3 009 vs 3 015, C2 2 240 vs 2 243 -- its wave-uniform branches
-// in every normalization cost SGPRs (12 -> 24 spilled into VGPR lanes on T).
-#ifndef RTW_SQRT_NORM
-#define RTW_SQRT_NORM 0
-#endif
-#if RTW_SQRT_NORM
-RTW_HD d3 normalize(d3 v) { return v / RTW_SQRT(len2(v)); }  // vec3.h:61-67
-#else
+// (normalize keeps the compiler's sqrt: sqrt_w's wave-uniform branch in
+// every normalization cost SGPRs, T -1.3 %)
 RTW_HD d3 normalize(d3 v) { return v / len(v); }  // vec3.h:61-67
-#endif
 // (the compiler's sqrt: in onb_from_w a wave-uniform branch inside the
 // frame's normalizations turned the onb into a scratch object)
 RTW_HD d3 normalize_b(d3 v) { return v / len(v); }
@@ -220,16 +177,10 @@ RTW_D uint32_t mr_next(uint32_t& s) {
 
 // The engine k steps ahead: x <- (48271^k mod m) x mod m, one multiply and
 // the same fold as mr_next (a product of two values below 2^31 folds to below
-// 2m, so one conditional subtract finishes it).  RTW_RNG_JUMP: the fp32-decided
-// rejection loops below test only the even draws of a try (the canonical
-// draws' leading terms), so a try jumps two draws at a time and the odd draws
-// are formed only where a try needs its exact fp64 point.
-// Measured (1 MI355X, A/B, profiles/r05/ab_r5c_*.log): T 4 607 vs 4 574,
-// C3 slice 3 058 vs 3 017, C2 2 258 vs 2 242, C5 ±0 alone (+4 % with
-// RTW_PACKET_ALL, below).
-#ifndef RTW_RNG_JUMP
-#define RTW_RNG_JUMP 1
-#endif
+// 2m, so one conditional subtract finishes it).  The fp32-decided rejection
+// loops below test only the even draws of a try (the canonical draws'
+// leading terms), so a try jumps two draws at a time and the odd draws are
+// formed only where a try needs its exact fp64 point (T +0.7 %, C3 +1.3 %).
 constexpr uint32_t kMrA = 48271u;
 constexpr uint32_t kMrA2 = 182605794u;  // 48271^2 mod (2^31 - 1)
 RTW_D uint32_t mr_jump(uint32_t s, uint32_t c) {
@@ -245,21 +196,11 @@ RTW_D double canon_raw(uint32_t r1, uint32_t r2) {
     const double e2 = (double)(r2 - 1u);
     double sum = 0.0 + e1 * 1.0;
     sum = sum + e2 * kCanonR;
-#ifndef RTW_CANON_ONESTEP
-#define RTW_CANON_ONESTEP 1
-#endif
-    // sum in [0, 2^62]: one Markstein step (rtw_div.h div_canon); 0: div_rcp's two
-    double r = RTW_CANON_ONESTEP ? div_canon(sum) : div_rcp(sum, kCanonDiv, kCanonRcp);
-    // RTW_CANON_MIN: libstdc++'s clamp (r >= 1 ? nextafter(1, 0) : r) as one
-    // v_min_f64 (r is never NaN: sum in [0, 2^62], a finite positive divisor;
-    // every r < 1 is <= nextafter(1, 0)) instead of a compare and two selects.
-    // Measured (1 MI355X, A/B, profiles/r05/ab_r5n_canon_min.log): T 4 740 vs
-    // 4 749 (its constant holds an SGPR pair through the loop), C2 / C3 / C5
-    // +-0.1 %.  Off.
-#ifndef RTW_CANON_MIN
-#define RTW_CANON_MIN 0
-#endif
-    return RTW_CANON_MIN ? __builtin_fmin(r, kOneMinusUlp) : (r >= 1.0 ? kOneMinusUlp : r);
+    // sum in [0, 2^62]: one Markstein step (rtw_div.h div_canon)
+    const double r = div_canon(sum);
+    // libstdc++'s clamp (as one v_min_f64: T -0.2 %, its constant holds an
+    // SGPR pair through the loop)
+    return r >= 1.0 ? kOneMinusUlp : r;
 }
 RTW_D double canon(uint32_t& s) {
     const uint32_t r1 = mr_next(s);
@@ -278,13 +219,6 @@ RTW_D uint64_t splitmix64(uint64_t x) {
 // rtw_path_seed (include/rtw_gpu.h); seed_mix = splitmix64(seed)
 RTW_D uint32_t path_seed(uint64_t seed_mix, uint32_t pixel, uint32_t s) {
     const uint64_t k = ((uint64_t)s << 32) ^ (uint64_t)pixel;
-// RTW_SEED_FOLD: the remainder as rtw_div.h's 32-bit fold (9 fewer VALU per
-// camera sample).  Measured (1 MI355X, A/B, profiles/r05/ab_r5o_seed_fold.log):
-// T 4 733 vs 4 744, C3 -0.5 %, T fp32 +0.6 %.  Off.
-#ifndef RTW_SEED_FOLD
-#define RTW_SEED_FOLD 0
-#endif
-    if (RTW_SEED_FOLD) return 1u + mod_2p31m2(splitmix64(seed_mix ^ k));  // (... % 2147483646)
     return (uint32_t)(1u + splitmix64(seed_mix ^ k) % 2147483646ull);
 }
 
@@ -294,7 +228,7 @@ RTW_D int random_int(uint32_t& s, int a, int b) {  // utility.h:22-25
 }
 
 // utility.h:27-35 — vec3(U, U, U) is built right to left by g++: z, y, x.
-// The rejection loop decided in fp32 (RTW_RIUS_FP32): a wave runs its
+// The rejection loop decided in fp32: a wave runs its
 // longest lane's number of tries (~4 for the metal lanes of a random_balls
 // wave, ~6 for the isotropic lanes of a Book-2 wave), so each try draws its
 // six raw values and tests 2 (e2 / R) - 1 -- the canonical draw's leading
@@ -303,11 +237,7 @@ RTW_D int random_int(uint32_t& s, int a, int b) {  // utility.h:22-25
 // test would, and a try in between takes the fp64 test.  The accepted try's
 // p is then formed from its raw draws in fp64, once: the same draws, the
 // same value, the same engine state as the reference's loop.
-#ifndef RTW_RIUS_FP32
-#define RTW_RIUS_FP32 1
-#endif
 RTW_D d3 random_in_unit_sphere(uint32_t& s) {
-#if RTW_RIUS_FP32
     constexpr float k2Rf = (float)(2.0 / kCanonR);  // 2 / R rounded
     auto lead = [&](uint32_t raw) { return __builtin_fmaf((float)(raw - 1u), k2Rf, -1.0f); };
     auto exact = [&](uint32_t z1, uint32_t z2, uint32_t y1, uint32_t y2, uint32_t x1, uint32_t x2) {
@@ -317,7 +247,6 @@ RTW_D d3 random_in_unit_sphere(uint32_t& s) {
         return d3{x, y, z} * 2.0 - d3{1.0, 1.0, 1.0};
     };
     uint32_t z1, z2, y1, y2, x1, x2;
-#if RTW_RNG_JUMP
     // a try is draws 1..6 from s0: the even ones by two-step jumps, the odd
     // ones (z1 = a s0, y1 = a z2, x1 = a y2) only where the point is formed
     uint32_t s0;
@@ -334,30 +263,7 @@ RTW_D d3 random_in_unit_sphere(uint32_t& s) {
         if (dot(q, q) < 1.0) break;
     }
     z1 = mr_jump(s0, kMrA), y1 = mr_jump(z2, kMrA), x1 = mr_jump(y2, kMrA);
-#else
-    for (;;) {
-        z1 = mr_next(s), z2 = mr_next(s);
-        y1 = mr_next(s), y2 = mr_next(s);
-        x1 = mr_next(s), x2 = mr_next(s);
-        const float px = lead(x2), py = lead(y2), pz = lead(z2);
-        const float d32 = __builtin_fmaf(px, px, __builtin_fmaf(py, py, pz * pz));
-        if (d32 < 1.0f - 0x1p-14f) break;
-        if (!(d32 < 1.0f + 0x1p-14f)) continue;
-        const d3 q = exact(z1, z2, y1, y2, x1, x2);
-        if (dot(q, q) < 1.0) break;
-    }
-#endif
     return exact(z1, z2, y1, y2, x1, x2);
-#else
-    d3 p;
-    do {
-        const double z = rnd01(s);
-        const double y = rnd01(s);
-        const double x = rnd01(s);
-        p = d3{x, y, z} * 2.0 - d3{1.0, 1.0, 1.0};
-    } while (dot(p, p) >= 1.0);
-    return p;
-#endif
 }
 
 RTW_D d3 random_cosine_direction(uint32_t& s) {  // utility.h:54-67
@@ -375,7 +281,7 @@ RTW_D d3 random_cosine_direction(uint32_t& s) {  // utility.h:54-67
 struct onb {
     d3 u, v, w;
 };
-// RTW_SQRT_UNIT: vectors whose length is known to be about 1 are normalised
+// Vectors whose length is known to be about 1 are normalised
 // with rtw_div.h's bare sqrt sequence (sqrt_core: the compiler's sqrt for x
 // >= 2^-766, without its range and class handling -- no branch, no vote):
 // the second axis of every frame (cross(w, a) with w unit and |w.x| <= 0.9
@@ -383,15 +289,10 @@ struct onb {
 // surface's normal (hit_record: (p - c) / r of a sphere, an axis normal,
 // rotated orthogonally; surf_frame::unit, a constant where shade_core builds
 // the frame -- a per-lane choice of the two forms made the frame a scratch
-// object).  A non-finite vector gives NaN either way.  0: the compiler's
-// sqrt (A/B).  Measured (1 MI355X, A/B, profiles/r05/ab_r5r_sqrt_unit.log;
-// bit-identical images, parity_r5r.log): T 4 762 vs 4 752, C3 +0.25 %, C2
-// and C5 +-0.
-#ifndef RTW_SQRT_UNIT
-#define RTW_SQRT_UNIT 1
-#endif
+// object).  A non-finite vector gives NaN either way.  T +0.25 %, C3 +0.25 %
+// (profiles/r05/ab_r5r_sqrt_unit.log).
 RTW_HD d3 normalize_unit(d3 v) {
-#if defined(__HIP_DEVICE_COMPILE__) && RTW_SQRT_CORE && RTW_SQRT_UNIT
+#if defined(__HIP_DEVICE_COMPILE__)
     return v / sqrt_core(len2(v));
 #else
     return normalize_b(v);
@@ -413,27 +314,11 @@ RTW_HD d3 local(const onb& b, d3 a) { return b.u * a.x + b.v * a.y + b.w * a.z; 
 // WORLD_RUN_YSPHERES: the same, all spheres for ysphere_scan.
 enum : int { WORLD_RUN_PLAIN = -1, WORLD_RUN_YSPHERES = -2 };
 struct bvh_node32;
-struct bvh_node16;
 // Device BVH node format (rtw_scene_upload writes it, node_at reads it):
-// 32-B nodes with fp32 bounds, or (RTW_NODE16) 16-B nodes with fp16 bounds
-// scaled by a power of two, so the LDS node packet holds twice the nodes.
-// Measured (1 MI355X, A/B, profiles/r04/ab_node16_r4e.log, ab_node16_r4f.log;
-// GPU suite green with it): C5 slice 613 vs 655, C3 2 684 vs 2 961, C3 fp32
-// 4 631 vs 5 156 Msamples/s.  The packet already holds all of C5's 1 668 and
-// C3's 969 nodes at 32 B (F_PIN), so only the decode is left: the slab test's
-// fp16 operands cost v_fma_mix_f32 at 4.4 cycles per wave instruction, or
-// v_cvt_f32_f16 at 4.3 + v_fma_f32 at 2.75 (converted bounds measured worse:
-// C3 2 582), against 2.75 for v_fma_f32 (profiles/r04/valu_rates_r4f.log).
-// Off; -DRTW_NODE16=1 selects it.  (fp32 Book 2, whose 32-B packet misses
-// ~230 nodes: 805 vs 843 Msamples/s, profiles/r05/ab_r5i_node16_fp32_rejected.log)
-#ifndef RTW_NODE16
-#define RTW_NODE16 0
-#endif
-#if RTW_NODE16
-using node_store = bvh_node16;
-#else
+// 32-B nodes with fp32 bounds.  (16-B fp16 nodes, twice the nodes per LDS
+// packet, measured C5 -6 %, C3 -9 %: the packet already holds every node of
+// C3 and C5 and the fp16 decode costs more)
 using node_store = bvh_node32;
-#endif
 struct world_run {
     int32_t entry, first_prim, n_prims, movers;  // movers: the prims hold DP_MOVING_COMMON*
 };
@@ -447,26 +332,17 @@ struct dev_entry {
     int32_t phase_material, bvh_root;
     int32_t n_outer_ops;  // MEDIUM: ops enclosing the medium (rtw_entry::n_outer_ops)
     int32_t movers;       // the group holds DP_MOVING_COMMON* spheres
-    int32_t bvh_root4;    // its BVH as 4-wide nodes (scene::nodes4), -1 none
+    int32_t pad;
     double neg_inv_density;  // MEDIUM: -(1 / density) (hittable.h:451), IEEE on the host at upload
 };
 struct dev_op {
     int32_t type, pad;
     double p[3];
 };
-// The media walk (scene::media) lists entries in visit order; a visit of a
-// medium visited twice also names a boundary cache slot (1-based, bits
-// 20-23) and, on its later visit, kVisitReuse: the boundary distances depend
-// only on the ray and the medium, so the second list walk reuses the first's.
-constexpr int kMediumSlots = 4;
-constexpr int32_t kVisitSlotShift = 20;
-constexpr int32_t kVisitEntry = (1 << kVisitSlotShift) - 1;
-constexpr int32_t kVisitReuse = 1 << 24;
-// Fused group walks (fused_group_bvh): the visit of a group BVH marked
-// kVisitFuse walks scene::fuse_entry's BVH too, in the same loop; that
-// entry's own visit (kVisitMerge) then merges the result found for it.
-constexpr int32_t kVisitFuse = 1 << 25;
-constexpr int32_t kVisitMerge = 1 << 26;
+// The media walk (scene::media) lists entry indices in visit order.
+// (A boundary cache for a medium's second visit measured C5 -8 %, and fused
+// walks of two group trees -11 %: DESIGN.md §4.2b.)
+constexpr int32_t kVisitEntry = (1 << 20) - 1;
 struct scene {
     const rtw_prim* prims;
     const dev_entry* entries;
@@ -492,8 +368,6 @@ struct scene {
     double mv_t0, mv_den;  // their time0 and time1 - time0
     int32_t fast_div;      // shared-divisor sphere roots allowed in world walks (ysphere_scan)
     double bvh_bound;      // largest |coordinate| of any device BVH node (make_slab_ray)
-    double node_scale;     // RTW_NODE16: a node's fp16 bounds are its coordinates / node_scale (a power of 2)
-    int32_t fuse_entry;    // the group BVH walked with the kVisitFuse visit's (-1: none)
     // ysphere_scan's fp32 prefilter: per prim {cx, cy, cz, dy, r^2, 0, 0, 0}
     // (r^2 = +inf: never filtered), and the largest |cx|, |cy|, |dy|, |cz|
     // and r^2 of the filtered spheres
@@ -506,14 +380,6 @@ struct scene {
     const node_store* lnodes;
     int32_t n_lnodes;
     int32_t n_nodes;  // device BVH nodes in all
-    // The same BVHs with 4-wide nodes (bvh_node4, rtw_scene_upload collapses
-    // the binary trees), walked by the persistent kernels with LDS stacks;
-    // nodes4 numbered breadth-first from all roots together like the binary
-    // ones, the top n_lnodes4 staged in LDS (lnodes4).  n_nodes4 = 0: none.
-    const struct bvh_node4* nodes4;
-    const int32_t* leaf4;  // per 4-wide leaf slot: first item | (count << 24)
-    const struct bvh_node4* lnodes4;
-    int32_t n_nodes4, n_lnodes4, world_root4;
 };
 
 // Scene features a traversal kernel is specialised for.
@@ -571,7 +437,7 @@ RTW_D T rd(const T* p) {
 struct entry_v {
     const dev_entry* p;
     const dev_op* ops;  // its op chain
-    int kind, first_prim, n_prims, n_ops, bvh_root, bvh_root4;
+    int kind, first_prim, n_prims, n_ops, bvh_root;
     bool movers;  // the group holds DP_MOVING_COMMON* spheres (dev_entry::movers)
 };
 template <bool U>
@@ -585,7 +451,6 @@ RTW_D entry_v view_entry(const scene& S, int i) {
     e.n_prims = rd<U>(&E[i].n_prims);
     e.n_ops = rd<U>(&E[i].n_ops);
     e.bvh_root = rd<U>(&E[i].bvh_root);
-    e.bvh_root4 = rd<U>(&E[i].bvh_root4);
     e.movers = rd<U>(&E[i].movers) != 0;
     return e;
 }
@@ -792,15 +657,12 @@ RTW_D rect_rcp make_rect_rcp(const scene& S, const ray& r) {
     return q;
 }
 // rect_axis_t with the walk's shared reciprocal of d.K.  BL (the world list
-// walk's rects, RTW_RECT_BRANCHLESS): the same comparisons without the early
+// walk's rects): the same comparisons without the early
 // return -- a and b formed for every lane, one branch level less of
 // exec-mask bookkeeping on the scalar unit per rect.  Measured (1 MI355X,
 // A/B, profiles/r05/ab_r5u_rect_branchless.log; bit-identical images): T
 // 4 811 vs 4 747 (+1.3 %); in the BVH leaves' box faces (mostly missed, the
 // early return skips their a, b) C5 -1.2 %, so those keep it.
-#ifndef RTW_RECT_BRANCHLESS
-#define RTW_RECT_BRANCHLESS 1
-#endif
 template <int K, int A, int B, bool BL = false>
 RTW_D bool rect_axis_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, double t0, double t1,
                          double& t_out) {
@@ -827,71 +689,12 @@ RTW_D bool rect_axis_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, do
     return true;
 }
 RTW_D bool rect_t_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, double t0, double t1, double& t_out) {
-    constexpr bool BL = RTW_RECT_BRANCHLESS != 0;  // (the world list walk's rects)
+    constexpr bool BL = true;  // (the world list walk's rects)
     if (q.type == RTW_PRIM_RECT_XY) return rect_axis_rcp<2, 0, 1, BL>(q, r, rr, t0, t1, t_out);
     if (q.type == RTW_PRIM_RECT_XZ) return rect_axis_rcp<1, 0, 2, BL>(q, r, rr, t0, t1, t_out);
     return rect_axis_rcp<0, 1, 2, BL>(q, r, rr, t0, t1, t_out);
 }
 
-#ifndef RTW_RECT_RCP
-#define RTW_RECT_RCP 1
-#endif
-
-// Two consecutive rects of a world run in parallel planes with the same
-// bounds (rtw_scene_upload marks the first with kRectPairHead: Cornell's
-// side walls, its ceiling and floor), in list order with the reference's
-// tests (hittable.h:149-257).  A plane whose quotient t = (k - o.K) / d.K
-// cannot reach t_min = 0.001 -- k - o.K of the other sign than d.K, or
-// |k - o.K| <= 0.00099 |d.K| -- is rejected by the range test whatever its
-// bounds, so a lane needs only the planes ahead of it: for an origin between
-// the planes (a ray inside the room) exactly one.  Every lane tests its one
-// plane in one instruction stream (same quotient, bounds test and
-// acceptance as rect_axis_rcp); lanes that need both (origin outside the
-// pair's slab) or whose d.K is 0 or not finite (a 0 / 0 quotient passes the
-// reference's range test) test both planes in list order in a branch that a
-// wave skips when none of its lanes needs it.  Two planes with distinct k
-// never give a lane equal t, so the winner is the list order's.
-// Measured (1 MI355X, A/B, profiles/r03/ab_rect_pairs_rejected.log): T
-// 4 243 vs 4 430 Msamples/s -- two of the twelve rect tests fewer, but the
-// pair's selects and branch raise the kernel's SGPR spills from 12 to 46.
-// Off; -DRTW_RECT_PAIRS=1 selects it.
-#ifndef RTW_RECT_PAIRS
-#define RTW_RECT_PAIRS 0
-#endif
-constexpr int32_t kRectPairHead = 0x40000000;  // in rtw_prim::flip (device copy only)
-template <int K, int A, int B>
-RTW_D void rect_pair_rcp(const rtw_prim& qa, const rtw_prim& qb, int ia, const ray& r, const rect_rcp& rr,
-                         double t_min, hit_state& h) {
-    const double oK = K == 0 ? r.o.x : (K == 1 ? r.o.y : r.o.z);
-    const double dK = K == 0 ? r.d.x : (K == 1 ? r.d.y : r.d.z);
-    const double na = qa.p[4] - oK, nb = qb.p[4] - oK;
-    const double lim = 0.00099 * __builtin_fabs(dK);
-    const bool ahead_a = ((na > 0 && dK > 0) || (na < 0 && dK < 0)) && __builtin_fabs(na) > lim;
-    const bool ahead_b = ((nb > 0 && dK > 0) || (nb < 0 && dK < 0)) && __builtin_fabs(nb) > lim;
-    const bool both = (ahead_a && ahead_b) || !(__builtin_fabs(dK) > 0 && __builtin_fabs(dK) < __builtin_inf()) ||
-                      na != na || nb != nb;  // a NaN origin: the reference accepts its NaN quotients
-    double t;
-    if (!both) {
-        rtw_prim qs = qa;  // the plane ahead (a when neither is: rejected by its range test)
-        qs.p[4] = ahead_b ? qb.p[4] : qa.p[4];
-        if (rect_axis_rcp<K, A, B>(qs, r, rr, t_min, h.t, t)) {
-            h.t = t;
-            h.prim = ahead_b ? ia + 1 : ia;
-            h.rect = true;
-        }
-    } else {
-        if (rect_axis_rcp<K, A, B>(qa, r, rr, t_min, h.t, t)) {
-            h.t = t;
-            h.prim = ia;
-            h.rect = true;
-        }
-        if (rect_axis_rcp<K, A, B>(qb, r, rr, t_min, h.t, t)) {
-            h.t = t;
-            h.prim = ia + 1;
-            h.rect = true;
-        }
-    }
-}
 
 // Linear closest hit over prims [first, first+n) of one group, in list order
 // (t range (t_min, closest]) with the reference's own comparisons; the
@@ -902,7 +705,7 @@ template <bool STATIC = false, bool WORLD = false>
 RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, bool movers) {
     const double fc = STATIC ? 0.0 : motion_frac(S, r.t, movers);
     const double a = dot(r.d, r.d);  // sphere.h:50, the same for every sphere
-    constexpr bool kRcp = WORLD && RTW_RECT_RCP;
+    constexpr bool kRcp = WORLD;
     rect_rcp rr;
     if (kRcp) rr = make_rect_rcp(S, r);
     for (int i = 0; i < n; ++i) {
@@ -928,16 +731,6 @@ RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_m
                     h.rect = false;
                 }
             }
-        } else if (kRcp && RTW_RECT_PAIRS && (q.flip & kRectPairHead)) {
-            // rects first + i, first + i + 1: parallel, the same bounds
-            const rtw_prim q2 = uprim(S.prims, first + i + 1);
-            if (q.type == RTW_PRIM_RECT_XY)
-                rect_pair_rcp<2, 0, 1>(q, q2, first + i, r, rr, t_min, h);
-            else if (q.type == RTW_PRIM_RECT_XZ)
-                rect_pair_rcp<1, 0, 2>(q, q2, first + i, r, rr, t_min, h);
-            else
-                rect_pair_rcp<0, 1, 2>(q, q2, first + i, r, rr, t_min, h);
-            ++i;
         } else {
             double t;
             if (kRcp ? rect_t_rcp(q, r, rr, t_min, h.t, t) : rect_t(q, r, t_min, h.t, t)) {
@@ -997,9 +790,6 @@ RTW_D double walk_quot(double num, double den, double y, bool ok) {
 #define RTW_YS_GROUP 4  // packed pairs filtered together per iteration (2: -1.7 %, 3: -2.5 %)
 #endif
 constexpr int kYsGroup = RTW_YS_GROUP;
-#ifndef RTW_YS_PACK
-#define RTW_YS_PACK 1  // the prefilter on packed fp32 pairs (rtw_scene_upload lays the records out for it)
-#endif
 constexpr int kYsAhead = RTW_YS_AHEAD;  // fp32 records in flight ahead of the filtered one
 RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, double fc) {
     const double a = dot(r.d, r.d);
@@ -1047,7 +837,6 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
             }
         }
     };
-#if RTW_YS_PACK
     // Two spheres per instruction: gfx950's packed fp32 VALU ops (v_pk_fma /
     // v_pk_mul / v_pk_add_f32) run the filter of spheres 2p and 2p + 1
     // side by side -- the same IEEE fp32 operations per sphere as the scalar
@@ -1113,32 +902,6 @@ RTW_D void ysphere_scan(const scene& S, int first, int n, const ray& r, double t
         const float d32 = __builtin_fmaf(b32, b32, -(af * (q32 - ld(g + 4))));
         if (__builtin_amdgcn_ballot_w64(!(d32 <= -E))) exact(n - 1);
     }
-#else
-    struct ysrec {
-        float cx, cy, cz, dy, rr;
-    };
-    auto load = [&](int i) {
-        const float* g = S.ysph + 8 * (size_t)(first + (i < n ? i : n - 1));
-        return ysrec{ld(g), ld(g + 1), ld(g + 2), ld(g + 3), ld(g + 4)};
-    };
-    ysrec ring[kYsAhead];
-#pragma unroll
-    for (int j = 0; j < kYsAhead; ++j) ring[j] = load(j);
-    for (int i0 = 0; i0 < n; i0 += kYsAhead) {
-#pragma unroll
-        for (int j = 0; j < kYsAhead; ++j) {
-            const int i = i0 + j;
-            if (i >= n) break;
-            const ysrec cur = ring[j];
-            ring[j] = load(i + kYsAhead);
-            const float ocx = oxf - cur.cx, ocy = oyf - __builtin_fmaf(cur.dy, fcf, cur.cy), ocz = ozf - cur.cz;
-            const float b32 = __builtin_fmaf(ocx, dxf, __builtin_fmaf(ocy, dyf, ocz * dzf));
-            const float q32 = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz));
-            const float d32 = __builtin_fmaf(b32, b32, -(af * (q32 - cur.rr)));
-            if (__builtin_amdgcn_ballot_w64(!(d32 <= -E))) exact(i);
-        }
-    }
-#endif
 }
 
 // Tie-exact test of prim `pi` against the running best, valid for ANY
@@ -1164,93 +927,10 @@ RTW_D void arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_sta
     }
 }
 
-// arbitrate with a wave-uniform prim index (packet walks): the prim's fields
-// are scalar loads, and the walk's shared 1 / dot(d, d) serves the sphere
-// roots (walk_quot's rules; t_min = 0.001)
-RTW_D void arbitrate_u(const scene& S, int pi, const ray& r, double t_min, hit_state& h, double fc, double ya,
-                       bool oka) {
-    const rtw_prim q = uprim(S.prims, pi);
-    const bool rl = !is_sphere(q.type);
-    double t;
-    if (rl) {
-        if (!rect_t(q, r, t_min, h.t, t)) return;
-    } else {
-        const d3 oc = r.o - sphere_center(q, r.t, fc);
-        const double a = dot(r.d, r.d);
-        const double b = dot(oc, r.d);
-        const double c = dot(oc, oc) - q.p[9];
-        const double disc = b * b - a * c;
-        if (!(disc > 0)) return;
-        const double sq = RTW_SQRT(disc);
-        t = walk_quot(-b - sq, a, ya, oka);
-        if (!(t < kDblMax && t > t_min)) {
-            t = walk_quot(-b + sq, a, ya, oka);
-            if (!(t < kDblMax && t > t_min)) return;
-        }
-        if (t > h.t) return;
-    }
-    if (better(t, pi, rl, h.t, h.prim, h.rect, h.prim != -1)) {
-        h.t = t;
-        h.prim = pi;
-        h.rect = rl;
-    }
-}
-
 // A box item of a group BVH (RTW_ITEM_BOX): its six rects in the box's list
 // order (hittable_list.h:65-114: +z, -z, +y, -y, +x, -x), each with the
 // reference's own test and better()'s tie rule -- exactly six arbitrate
 // calls, with each rect's plane axis known instead of read from its type.
-// (U: the box index is wave-uniform, a packet walk's: the rects' fields are
-// scalar loads)
-template <int K, int A, int B, bool U = false>
-RTW_D void rect_arbitrate(const scene& S, int pi, const ray& r, double t_min, hit_state& h) {
-    double t;
-    if constexpr (U) {
-        const rtw_prim q = uprim(S.prims, pi);
-        if (!rect_axis_t<K, A, B>(q, r, t_min, h.t, t)) return;
-    } else {
-        const rtw_prim& q = S.prims[pi];  // fields read where the test uses them
-        if (!rect_axis_t<K, A, B>(q, r, t_min, h.t, t)) return;
-    }
-    if (better(t, pi, true, h.t, h.prim, h.rect, h.prim != -1)) {
-        h.t = t;
-        h.prim = pi;
-        h.rect = true;
-    }
-}
-// A rect of plane axis K whose quotient t = (k - o.K) / d.K lies above h.t
-// is rejected by rect_axis_t's `t > t1` now and for every later (smaller)
-// h.t, so skipping it changes nothing.  That is certain without the division
-// when n = k - o.K (the test's own numerator) lies beyond
-// p2 = fl(fl(h.t d.K) (1 + 2^-50)) on d.K's side and |fl(h.t d.K)| > 2^-1000:
-// then |p2| >= |h.t d.K| (1 + 2^-51), so n / d.K > h.t (1 + 2^-51) >=
-// h.t + ulp(h.t) and the correctly rounded quotient is above h.t.  A zero or
-// NaN d.K, or an infinite product, is never skipped.
-template <int K, int A, int B>
-RTW_D void rect_arbitrate_far(const scene& S, int pi, const ray& r, double t_min, hit_state& h) {
-    const double ok = K == 0 ? r.o.x : (K == 1 ? r.o.y : r.o.z);
-    const double od = K == 0 ? r.d.x : (K == 1 ? r.d.y : r.d.z);
-    const double n = S.prims[pi].p[4] - ok;
-    const double p = h.t * od;
-    const double p2 = p * (1.0 + 0x1p-50);
-    const bool beyond = __builtin_fabs(p) > 0x1p-1000 && (od > 0 ? n > p2 : n < p2);
-    if (!beyond) rect_arbitrate<K, A, B>(S, pi, r, t_min, h);
-}
-// Box items test the face of each pair the ray can enter through first (the
-// lower plane when d.K > 0, of a box built with p0 <= p1; the pair's first
-// rect otherwise) and then the other three through rect_arbitrate_far: once
-// the ray has hit a near face, the far faces lie beyond it and cost no
-// division.  better() makes the winner independent of the test order
-// (its ties follow the list index, not the visiting order), and a skipped
-// rect could never have been accepted, so the result is box_arbitrate's in
-// list order exactly, whatever the box's orientation.  Measured (1 MI355X,
-// A/B, profiles/r03/ab_box_near_rejected.log): C5 slice 619.0 vs 621.9
-// Msamples/s (the C5 walk is bound by node-load latency and divergence, not
-// by the boxes' divisions; two more VGPR spills); GPU parity suite green with
-// it on.  Off; -DRTW_BOX_NEAR=1 selects it.
-#ifndef RTW_BOX_NEAR
-#define RTW_BOX_NEAR 0
-#endif
 // A box's six rect tests divide by only three values, d.x, d.y and d.z
 // (each face pair shares its plane axis), so a box computes the three
 // reciprocals once (rtw_div.h rcp_hw) and each face's t = (k - o.K) / d.K
@@ -1259,9 +939,6 @@ RTW_D void rect_arbitrate_far(const scene& S, int pi, const ray& r, double t_min
 // 2^40, |d.K| in [2^-200, 2^200]) when t_min >= 0.001 (a numerator below
 // 2^-800 then gives quotients that t_min rejects alike); other lanes, and
 // boxes probed as a medium's boundary (t_min = -DBL_MAX), divide exactly.
-#ifndef RTW_BOX_RCP
-#define RTW_BOX_RCP 1
-#endif
 template <int K, int A, int B>
 RTW_D void rect_arbitrate_rcp(const scene& S, int pi, const ray& r, const rect_rcp& rr, double t_min, hit_state& h) {
     double t;
@@ -1273,15 +950,6 @@ RTW_D void rect_arbitrate_rcp(const scene& S, int pi, const ray& r, const rect_r
         h.rect = true;
     }
 }
-// the six faces with the reciprocals of a leaf (leaf_items)
-RTW_D void box_arbitrate_rr(const scene& S, int first, const ray& r, const rect_rcp& rr, double t_min, hit_state& h) {
-    rect_arbitrate_rcp<2, 0, 1>(S, first, r, rr, t_min, h);
-    rect_arbitrate_rcp<2, 0, 1>(S, first + 1, r, rr, t_min, h);
-    rect_arbitrate_rcp<1, 0, 2>(S, first + 2, r, rr, t_min, h);
-    rect_arbitrate_rcp<1, 0, 2>(S, first + 3, r, rr, t_min, h);
-    rect_arbitrate_rcp<0, 1, 2>(S, first + 4, r, rr, t_min, h);
-    rect_arbitrate_rcp<0, 1, 2>(S, first + 5, r, rr, t_min, h);
-}
 // make_rect_rcp with the quotient rule's t_min condition folded in
 RTW_D rect_rcp make_rect_rcp_t(const scene& S, const ray& r, double t_min) {
     rect_rcp rr = make_rect_rcp(S, r);
@@ -1290,35 +958,14 @@ RTW_D rect_rcp make_rect_rcp_t(const scene& S, const ray& r, double t_min) {
     for (int k = 0; k < 3; ++k) rr.ok[k] = rr.ok[k] && tmin_ok;
     return rr;
 }
-template <bool U = false>
 RTW_D void box_arbitrate(const scene& S, int first, const ray& r, double t_min, hit_state& h) {
-    if constexpr (RTW_BOX_RCP && !RTW_BOX_NEAR && !U) {
-        const rect_rcp rr = make_rect_rcp_t(S, r, t_min);
-        rect_arbitrate_rcp<2, 0, 1>(S, first, r, rr, t_min, h);
-        rect_arbitrate_rcp<2, 0, 1>(S, first + 1, r, rr, t_min, h);
-        rect_arbitrate_rcp<1, 0, 2>(S, first + 2, r, rr, t_min, h);
-        rect_arbitrate_rcp<1, 0, 2>(S, first + 3, r, rr, t_min, h);
-        rect_arbitrate_rcp<0, 1, 2>(S, first + 4, r, rr, t_min, h);
-        rect_arbitrate_rcp<0, 1, 2>(S, first + 5, r, rr, t_min, h);
-        return;
-    }
-    if constexpr (RTW_BOX_NEAR && !U) {
-        const int nz = first + (r.d.z > 0), ny = first + 2 + (r.d.y > 0), nx = first + 4 + (r.d.x > 0);
-        const int pair = 2 * first + 1;  // (first + 2j) + (first + 2j + 1) - 4j
-        rect_arbitrate<2, 0, 1>(S, nz, r, t_min, h);
-        rect_arbitrate<1, 0, 2>(S, ny, r, t_min, h);
-        rect_arbitrate<0, 1, 2>(S, nx, r, t_min, h);
-        rect_arbitrate_far<2, 0, 1>(S, pair - nz, r, t_min, h);
-        rect_arbitrate_far<1, 0, 2>(S, pair + 4 - ny, r, t_min, h);
-        rect_arbitrate_far<0, 1, 2>(S, pair + 8 - nx, r, t_min, h);
-        return;
-    }
-    rect_arbitrate<2, 0, 1, U>(S, first, r, t_min, h);
-    rect_arbitrate<2, 0, 1, U>(S, first + 1, r, t_min, h);
-    rect_arbitrate<1, 0, 2, U>(S, first + 2, r, t_min, h);
-    rect_arbitrate<1, 0, 2, U>(S, first + 3, r, t_min, h);
-    rect_arbitrate<0, 1, 2, U>(S, first + 4, r, t_min, h);
-    rect_arbitrate<0, 1, 2, U>(S, first + 5, r, t_min, h);
+    const rect_rcp rr = make_rect_rcp_t(S, r, t_min);
+    rect_arbitrate_rcp<2, 0, 1>(S, first, r, rr, t_min, h);
+    rect_arbitrate_rcp<2, 0, 1>(S, first + 1, r, rr, t_min, h);
+    rect_arbitrate_rcp<1, 0, 2>(S, first + 2, r, rr, t_min, h);
+    rect_arbitrate_rcp<1, 0, 2>(S, first + 3, r, rr, t_min, h);
+    rect_arbitrate_rcp<0, 1, 2>(S, first + 4, r, rr, t_min, h);
+    rect_arbitrate_rcp<0, 1, 2>(S, first + 5, r, rr, t_min, h);
 }
 // a group-BVH leaf item: a prim, or a box's six rects
 RTW_D void arbitrate_item(const scene& S, int it, const ray& r, double t_min, hit_state& h, double fc) {
@@ -1327,15 +974,6 @@ RTW_D void arbitrate_item(const scene& S, int it, const ray& r, double t_min, hi
     else
         arbitrate(S, it, r, t_min, h, fc);
 }
-// ... with a wave-uniform item (packet walks); arbitrate_u without a shared
-// reciprocal divides exactly, as arbitrate does
-RTW_D void arbitrate_item_u(const scene& S, int it, const ray& r, double t_min, hit_state& h, double fc) {
-    if (it & RTW_ITEM_BOX)
-        box_arbitrate<true>(S, it & RTW_ITEM_INDEX, r, t_min, h);
-    else
-        arbitrate_u(S, it, r, t_min, h, fc, 0.0, false);
-}
-
 // arbitrate for a world walk's one-prim leaves with the walk's shared
 // 1 / dot(d, d) (walk_quot's rules; t_min = 0.001)
 RTW_D void arbitrate_a(const scene& S, int pi, const ray& r, double t_min, hit_state& h, double fc, double ya,
@@ -1367,45 +1005,10 @@ RTW_D void arbitrate_a(const scene& S, int pi, const ray& r, double t_min, hit_s
     }
 }
 
-// The items of a group-BVH leaf, with reciprocals shared across the leaf:
-// the three of the ray's direction for its boxes' faces (box_arbitrate's rule)
-// and 1 / dot(d, d) for its spheres' roots (arbitrate_a's), each computed
-// only when one of the wave's leaves holds such an item.  Quotients are
-// bit-identical under the rules of make_rect_rcp / walk_quot with t_min >=
-// 0.001; other lanes (and boundary probes) divide exactly.
-// Measured (profiles/r04/ab_cache_leafrcp.log): C5 slice -8 % with the
-// medium cache, -7 % without it (the kernel spills 29 VGPRs instead of 19):
-// off; -DRTW_LEAF_RCP=1 selects it.
-#ifndef RTW_LEAF_RCP
-#define RTW_LEAF_RCP 0
-#endif
+// The items of a group-BVH leaf.  (Reciprocals shared across the leaf's
+// boxes and spheres measured C5 -7 %: 10 more spilled VGPRs, §4.2b.)
 RTW_D void leaf_items(const scene& S, int la, int lc, const ray& r, double t_min, hit_state& h, double fc) {
-    if constexpr (!RTW_LEAF_RCP || RTW_BOX_NEAR) {
-        for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
-        return;
-    }
-    bool box = false, sph = false;
-    for (int k = 0; k < lc; ++k) {
-        const int it = S.items[la + k];
-        box = box || (it & RTW_ITEM_BOX);
-        sph = sph || !(it & RTW_ITEM_BOX);
-    }
-    rect_rcp rr{};
-    double ya = 0.0;
-    bool oka = false;
-    if (box) rr = make_rect_rcp_t(S, r, t_min);
-    if (sph) {
-        const double a = dot(r.d, r.d);
-        ya = rcp_hw(a);
-        oka = t_min >= kTMin && walk_ray_ok(S, r, fc) && div_hw_ok_b(a);
-    }
-    for (int k = 0; k < lc; ++k) {
-        const int it = S.items[la + k];
-        if (it & RTW_ITEM_BOX)
-            box_arbitrate_rr(S, it & RTW_ITEM_INDEX, r, rr, t_min, h);
-        else
-            arbitrate_a(S, it, r, t_min, h, fc, ya, oka);
-    }
+    for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
 }
 
 // Device BVH node (rtw_scene_upload): the builder's padded fp64 bounds
@@ -1418,29 +1021,6 @@ struct bvh_node32 {
     int32_t b;  // inner: right child | pad << 28 (push_children); leaf: -count
 };
 RTW_HD int node_count(const bvh_node32& n) { return n.b < 0 ? -n.b : 0; }
-// The 16-B form (RTW_NODE16): bounds as fp16 of coordinate * 2^k (rounded
-// outward at upload; scene::node_scale = 2^-k), w = index (24 bits) | meta
-// << 24: a leaf's first item and meta 0x80 | count (count < 128); an inner
-// node's left child -- the right one is the next node (breadth-first
-// numbering puts siblings together) -- and meta = its split bits (pad).
-struct bvh_node16 {
-    uint16_t lo[3], hi[3];
-    uint32_t w;
-};
-constexpr uint32_t kNode16Leaf = 0x80u;
-// the 16-B node as the walks read it: fp32 bounds in the scaled space (the
-// slab ray's reciprocals carry node_scale), children / items as bvh_node32's
-RTW_D float half_bits(uint32_t h) { return (float)__builtin_bit_cast(_Float16, (uint16_t)h); }
-RTW_D bvh_node32 decode16(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
-    bvh_node32 nd;
-    nd.lo[0] = half_bits(x & 0xffff), nd.lo[1] = half_bits(x >> 16), nd.lo[2] = half_bits(y & 0xffff);
-    nd.hi[0] = half_bits(y >> 16), nd.hi[1] = half_bits(z & 0xffff), nd.hi[2] = half_bits(z >> 16);
-    const int idx = (int)(w & 0xffffffu), meta = (int)(w >> 24);
-    nd.a = idx;
-    nd.b = (meta & kNode16Leaf) ? -(meta & 0x7f) : ((idx + 1) | (meta << 28));
-    return nd;
-}
-
 // Per-walk fp32 form of the ray for the slab tests: t = x * inv + oi per
 // axis, with oi = -o * inv moved down (oin, near planes) and up (oif, far
 // planes) by eps = (2^-21 + 2^-22) (B + |o|) |inv| + 2^-120, B the largest
@@ -1452,15 +1032,12 @@ RTW_D bvh_node32 decode16(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
 // off by less than 2^-23.9 of that), and 2^-120 a flushed denormal result.
 // An axis whose |inv| or eps exceeds 2^90 (d.K ~ 0, NaN) never culls:
 // inv = 0, oin = -inf, oif = +inf.
-// RTW_SLAB_RCP32: inv is the hardware fp32 reciprocal of fl32(d) instead of
+// inv is the hardware fp32 reciprocal of fl32(d) instead of
 // fl32(1.0 / d) -- within 2^-22.4 |1 / d| (2^-24 for the conversion, 1 ulp
 // for v_rcp_f32), and oi = -o * inv in fp64 within 2^-22.4 |o / d|; with the
 // final rounding of oi +- eps that is under 2^-21.9 (B + |o|) |1 / d|, inside
 // the 2^-21 part (eps itself computed from |inv| loses a 2^-22 relative) --
 // three fp64 divisions fewer per walk.
-#ifndef RTW_SLAB_RCP32
-#define RTW_SLAB_RCP32 1
-#endif
 struct slab_ray {
     float inv[3], oin[3], oif[3];
 };
@@ -1469,24 +1046,11 @@ RTW_D slab_ray make_slab_ray(const scene& S, const ray& r) {
     const double dd[3] = {r.d.x, r.d.y, r.d.z}, oo[3] = {r.o.x, r.o.y, r.o.z};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-#if RTW_SLAB_RCP32
         const double inv = (double)__builtin_amdgcn_rcpf((float)dd[k]);
-#else
-        const double inv = 1.0 / dd[k];
-#endif
         const double oi = -oo[k] * inv;
         const double eps = 0x1.8p-21 * (S.bvh_bound + __builtin_fabs(oo[k])) * __builtin_fabs(inv) + 0x1p-120;
-#if RTW_NODE16
-        // node coordinates x = h * node_scale: x * inv = h * (inv * node_scale)
-        // exactly while inv * node_scale stays a normal float (power-of-2 scale)
-        const double invs = inv * S.node_scale;
-        const bool ok = __builtin_fabs(inv) <= 0x1p90 && eps <= 0x1p90 && __builtin_fabs(invs) <= 0x1p100 &&
-                        __builtin_fabs(invs) >= 0x1p-100;
-        s.inv[k] = ok ? (float)invs : 0.0f;
-#else
         const bool ok = __builtin_fabs(inv) <= 0x1p90 && eps <= 0x1p90;
         s.inv[k] = ok ? (float)inv : 0.0f;
-#endif
         s.oin[k] = ok ? (float)(oi - eps) : -__builtin_inff();
         s.oif[k] = ok ? (float)(oi + eps) : __builtin_inff();
     }
@@ -1521,20 +1085,7 @@ RTW_D bool slab32(const bvh_node32& nd, const slab_ray& s, float t0, float t1) {
 // a world-BVH leaf) share one stack above the outer walk's entries; the host
 // checks at upload that the deepest nesting fits (rtw_scene_upload).
 constexpr int kStack = 48;
-// Measured (1 MI355X, A/B against the binary child-test / while-while
-// walks, profiles/r03/ab_bvh4_rejected.log): C3 slice 2 592 vs 2 611
-// Msamples/s, C5 slice 545 vs 599.  On C3 it issues 8.6 % fewer VALU and
-// 15 % fewer SALU / LDS instructions per segment but 40 % more global
-// loads (a 4-wide node is 112 bytes: the LDS packet holds three levels
-// instead of eight) and 15 % more issue stalls, for the same time; the C5
-// kernel spills 25 VGPRs (6 before).  Off; -DRTW_BVH4=1 selects it.
-#ifndef RTW_BVH4
-#define RTW_BVH4 0
-#endif
-#ifndef RTW_LDS_STACK
-#define RTW_LDS_STACK (RTW_BVH4 ? 20 : 16)  // 4-wide walks push up to three children per level
-#endif
-constexpr int kLdsStack = RTW_LDS_STACK;
+constexpr int kLdsStack = 16;  // LDS stack entries per lane
 struct local_stack {
     static constexpr int cap = kStack;
     int s[kStack];
@@ -1556,11 +1107,6 @@ struct lds_stack {  // 16-bit node indices (LDS stacks need < 65536 nodes: uploa
     static constexpr int cap = kLdsStack;
     uint16_t* p;  // &column[0][lane]; entry i at p[i * kPBlock]
     RTW_D uint16_t& at(int i) { return p[i * kPBlock]; }
-    // a packet walk's wave-uniform stack: row 0 of the wave's 64 columns
-    static constexpr int wave_cap = 64;
-    RTW_D uint16_t* wave_row() const {
-        return p - __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    }
 };
 
 // A BVH node: from the LDS packet when it is one of the top n_lnodes, else
@@ -1572,16 +1118,8 @@ RTW_D bvh_node32 node_at(const scene& S, int i) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     using lds_v4 = const __attribute__((address_space(3))) v4u;
     using glb_v4 = const __attribute__((address_space(1))) v4u;
-#if RTW_NODE16
-    v4u a;
-    if (i < S.n_lnodes)
-        a = *(lds_v4*)(S.lnodes + i);
-    else
-        a = *(glb_v4*)(S.nodes + i);
-    return decode16(a.x, a.y, a.z, a.w);
-#else
     v4u a, b;
-    if (RTW_PACKET_ALL && S.n_lnodes >= S.n_nodes) {
+    if (S.n_lnodes >= S.n_nodes) {
         // every node is in the packet (wave-uniform: a scalar branch, no
         // per-lane address-space test; Book 2's 1 668 nodes with F_PIN)
         lds_v4* p = (lds_v4*)(S.lnodes + i);
@@ -1598,60 +1136,6 @@ RTW_D bvh_node32 node_at(const scene& S, int i) {
     __builtin_memcpy(&nd, &a, 16);
     __builtin_memcpy(reinterpret_cast<char*>(&nd) + 16, &b, 16);
     return nd;
-#endif
-}
-
-// 4-wide BVH node (rtw_scene_upload collapses each binary tree: a node's
-// slots are its binary children, the largest-area inner ones opened once
-// more until there are four), bounds per axis for the four slots so each
-// 16-byte load brings one plane of all four boxes (and pairs of slots sit in
-// adjacent registers for the packed fp32 slab test).  child[c] >= 0: inner
-// node4; kNoChild: an unused slot; other values < 0: leaf ~l
-// (scene::leaf4[l]).  The walks read the first 112 bytes.
-constexpr int32_t kNoChild = INT32_MIN;
-struct bvh_node4 {
-    float lo[3][4], hi[3][4];
-    int32_t child[4];
-    int32_t pad[4];
-};
-static_assert(sizeof(bvh_node4) == 128, "bvh_node4 layout");
-
-RTW_D bvh_node4 node4_at(const scene& S, int i) {
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    using lds_v4 = const __attribute__((address_space(3))) v4u;
-    using glb_v4 = const __attribute__((address_space(1))) v4u;
-    v4u a[7];
-    if (i < S.n_lnodes4) {
-        lds_v4* p = (lds_v4*)(S.lnodes4 + i);
-#pragma unroll
-        for (int k = 0; k < 7; ++k) a[k] = p[k];
-    } else {
-        glb_v4* p = (glb_v4*)(S.nodes4 + i);
-#pragma unroll
-        for (int k = 0; k < 7; ++k) a[k] = p[k];
-        asm volatile("" ::"v"(a[0].x));  // global loads, not one flat load (node_at)
-    }
-    bvh_node4 nd;
-    __builtin_memcpy(&nd, a, 112);
-    nd.pad[0] = nd.pad[1] = nd.pad[2] = nd.pad[3] = 0;
-    return nd;
-}
-
-// A node at a wave-uniform index (packet walks): scalar loads through the
-// scalar cache, the fields land in SGPRs.
-RTW_D bvh_node32 node_s(const scene& S, int i) {
-#if RTW_NODE16
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(S.nodes + i);
-    return decode16(ld(p), ld(p + 1), ld(p + 2), ld(p + 3));
-#else
-    bvh_node32 nd;
-    const bvh_node32* p = S.nodes + i;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) nd.lo[k] = ld(&p->lo[k]), nd.hi[k] = ld(&p->hi[k]);
-    nd.a = ld(&p->a);
-    nd.b = ld(&p->b);
-    return nd;
-#endif
 }
 
 // Inner nodes carry their children's split axis (pad & 3) and whether the
@@ -1670,31 +1154,12 @@ RTW_D void push_children(const bvh_node32& nd, int dneg, STK& stk, int& sp) {
     stk.at(sp++) = left_first ? nd.a : right;
 }
 
-#ifndef RTW_CHILD_TEST
-#define RTW_CHILD_TEST 1
-#endif
 // Speculative while-while for the world child-test walk (Aila & Laine 2009):
 // lanes that already hold their leaf keep walking until every lane of the
 // wave has one, so the inner loop runs with more lanes busy.  Nodes are then
 // sometimes tested against a closest t the pending leaf would have
 // tightened: more work per lane, never a different winner (better() makes
 // it order-independent).
-#ifndef RTW_SPEC_WALK
-#define RTW_SPEC_WALK 1
-#endif
-// ... and for the group BVH walks (while-while form)
-// RTW_GROUP_TOS: the group walks keep the nearer child in a register instead
-// of pushing and popping it through the LDS stack (below; rtw_fast.h's group
-// and world walks likewise).  Measured (1 MI355X, A/B,
-// profiles/r05/ab_r5d_*.log): C5 slice 671 vs 709, C3 fp32 4 652 vs 5 191,
-// C5 fp32 812 vs 846 -- the per-lane select between register and stack and
-// the masked stack read cost more than the LDS round trip.  Off.
-#ifndef RTW_GROUP_TOS
-#define RTW_GROUP_TOS 0
-#endif
-#ifndef RTW_SPEC_GROUP
-#define RTW_SPEC_GROUP 0
-#endif
 
 RTW_D double widen_lo(double t) { return t > 0 ? t * 0.5 : t * 2.0 - 1e-9; }
 RTW_D double widen_hi(double t) { return t * (1 + 1e-12) + 1e-9; }
@@ -1709,7 +1174,7 @@ RTW_D float t_hi32(double t) {
     return __builtin_fmaf(__builtin_fabsf(f), 0x1p-23f, f) + 0x1p-126f;
 }
 
-// One step of the child-test walks (RTW_CHILD_TEST): the inner node (ca, cb)
+// One step of the child-test walks: the inner node (ca, cb)
 // (its a / b fields) loads both children and slab-tests them together; the
 // nearer passing child becomes (ca, cb), the other passing one is stacked.
 // Returns false when neither passes.
@@ -1717,23 +1182,7 @@ template <class STK>
 RTW_D bool expand_children(const scene& S, const slab_ray& sr, float t0, float t1, int dneg, STK& stk, int& sp,
                            int& ca, int& cb) {
     const int pad = cb >> 28, right = cb & 0x0fffffff;
-#if RTW_NODE16
-    // siblings are adjacent 16-B nodes: one 32-B read for both
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    using lds_v4 = const __attribute__((address_space(3))) v4u;
-    using glb_v4 = const __attribute__((address_space(1))) v4u;
-    v4u qa, qb;
-    if (right < S.n_lnodes) {
-        lds_v4* p = (lds_v4*)(S.lnodes + ca);
-        qa = p[0], qb = p[1];
-    } else {
-        glb_v4* p = (glb_v4*)(S.nodes + ca);
-        qa = p[0], qb = p[1];
-    }
-    const bvh_node32 L = decode16(qa.x, qa.y, qa.z, qa.w), R = decode16(qb.x, qb.y, qb.z, qb.w);
-#else
     const bvh_node32 L = node_at(S, ca), R = node_at(S, right);
-#endif
     const bool hl = slab32(L, sr, t0, t1), hr = slab32(R, sr, t0, t1);
     const bool left_first = (((dneg >> (pad & 3)) ^ (pad >> 2)) & 1) == 0;
     const bool hn = left_first ? hl : hr, hf = left_first ? hr : hl;
@@ -1746,235 +1195,21 @@ RTW_D bool expand_children(const scene& S, const slab_ray& sr, float t0, float t
     return hn || hf;
 }
 
-// slab32 for the four slots of a bvh_node4 at once: the near / far plane
-// values of slot pairs {0, 1} and {2, 3} come from packed fp32 fmas (one
-// v_pk_fma_f32 per two slots, the same IEEE operation per slot as slab32's,
-// so its conservative bound holds per slot); tn[c] is the slot's entry t.
-RTW_D void slab4(const bvh_node4& nd, const slab_ray& s, float t0, float t1, float tn[4], bool pass[4]) {
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    f2 n01 = t0, n23 = t0, f01 = t1, f23 = t1;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const f2 inv = s.inv[k], oin = s.oin[k], oif = s.oif[k];
-        const f2 lo01 = {nd.lo[k][0], nd.lo[k][1]}, lo23 = {nd.lo[k][2], nd.lo[k][3]};
-        const f2 hi01 = {nd.hi[k][0], nd.hi[k][1]}, hi23 = {nd.hi[k][2], nd.hi[k][3]};
-        const f2 an01 = __builtin_elementwise_fma(lo01, inv, oin), bn01 = __builtin_elementwise_fma(hi01, inv, oin);
-        const f2 af01 = __builtin_elementwise_fma(lo01, inv, oif), bf01 = __builtin_elementwise_fma(hi01, inv, oif);
-        const f2 an23 = __builtin_elementwise_fma(lo23, inv, oin), bn23 = __builtin_elementwise_fma(hi23, inv, oin);
-        const f2 af23 = __builtin_elementwise_fma(lo23, inv, oif), bf23 = __builtin_elementwise_fma(hi23, inv, oif);
-        n01 = __builtin_elementwise_max(n01, __builtin_elementwise_min(an01, bn01));
-        n23 = __builtin_elementwise_max(n23, __builtin_elementwise_min(an23, bn23));
-        f01 = __builtin_elementwise_min(f01, __builtin_elementwise_max(af01, bf01));
-        f23 = __builtin_elementwise_min(f23, __builtin_elementwise_max(af23, bf23));
-    }
-    tn[0] = n01.x, tn[1] = n01.y, tn[2] = n23.x, tn[3] = n23.y;
-    pass[0] = n01.x <= f01.x && nd.child[0] != kNoChild;
-    pass[1] = n01.y <= f01.y && nd.child[1] != kNoChild;
-    pass[2] = n23.x <= f23.x && nd.child[2] != kNoChild;
-    pass[3] = n23.y <= f23.y && nd.child[3] != kNoChild;
-}
-
-// Walk of a 4-wide BVH from node4 `root` (its own box is not tested: its
-// slots are), while-while as the binary walks: every lane expands nodes --
-// continuing with its nearest passing slot, stacking the other passing ones
-// -- until it holds a leaf (or its stack runs dry), then all lanes test their
-// leaves together with leaf(first_item, count).  Stacked slots are not
-// re-tested when popped (the leaf tests and the next expansion cull with the
-// closest t of that time).  The stack above `base` holds node4 indices and
-// ~leaf (16-bit: upload checks both spaces and the depth).  Visiting order
-// never changes a lane's result: better() (arbitrate) reproduces the list
-// order's tie rule.
-template <class STK, class LEAF>
-RTW_D void walk4(const scene& S, int root, const slab_ray& sr, float t0, const hit_state& h, STK& stk, int base,
-                 LEAF&& leaf) {
-    int sp = base;
-    int cur = root;  // the node4 this lane expands next, -1: pop one
-    for (;;) {
-        int la = 0, lc = 0;  // this lane's pending leaf
-        while (lc == 0) {
-            int lf = -1;  // a leaf reached: its leaf4 index
-            if (cur < 0) {
-                if (sp == base) break;
-                const int e = (int16_t)stk.at(--sp);
-                if (e >= 0)
-                    cur = e;
-                else
-                    lf = ~e;
-            }
-            if (cur >= 0) {
-                const bvh_node4 nd = node4_at(S, cur);
-                float tn[4];
-                bool pass[4];
-                slab4(nd, sr, t0, t_hi32(h.t), tn, pass);
-                int best = -1;
-                float bt = __builtin_inff();
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (pass[c] && tn[c] < bt) best = c, bt = tn[c];
-                // the others, farthest slot last pushed ... popped first
-#pragma unroll
-                for (int c = 3; c >= 0; --c)
-                    if (pass[c] && c != best && sp < STK::cap)  // always fits: depth checked at upload
-                        stk.at(sp++) = (uint16_t)nd.child[c];
-                cur = -1;
-                if (best >= 0) {
-                    const int ch = best == 0 ? nd.child[0] : best == 1 ? nd.child[1] : best == 2 ? nd.child[2] : nd.child[3];
-                    if (ch >= 0)
-                        cur = ch;
-                    else
-                        lf = ~ch;
-                }
-            }
-            if (lf >= 0) {
-                const int v = S.leaf4[lf];
-                la = v & 0xffffff;
-                lc = v >> 24;
-            }
-        }
-        if (lc == 0) break;
-        leaf(la, lc);
-    }
-}
-
-// Packet walk of one BVH from a wave-uniform root: the wave walks the tree
-// together.  A node is visited when its box passes the slab test of at least
-// one lane (each lane with its own closest t), so the node index, the stack
-// and the leaf items are wave-uniform: nodes, items and prims come in by
-// scalar loads, the stack is one LDS row per wave, and every lane's slab test
-// runs in the same instruction (a per-lane walk left two thirds of the lanes
-// idle while the wave's longest walk finished).  A leaf's exact tests run on
-// the lanes whose slab test passed (leaf(first, count) is called under that
-// mask).  Inner nodes continue with the child most passing lanes would visit
-// first and stack the other.  Each lane gets its own walk's result: every node
-// its own walk would enter with a given closest t passes its test here with
-// the same or a larger t (t only shrinks), leaves it would skip cannot beat
-// its closest hit, and better() makes the winner independent of the order.
-// Measured (1 MI355X, A/B against the per-lane walks): C3 slice 1 665 vs
-// 2 572 Msamples/s, C5 slice 318 vs 597 (profiles/r03/ab_packet_rejected.log).
-// Every node is one dependent scalar load -> slab test -> ballot -> branch
-// step, ~100 of them per wave-iteration on C3, and four waves per SIMD do
-// not hide that chain; per-lane walks keep 64 loads in flight per
-// instruction.  Off; -DRTW_PACKET=1 / -DRTW_PACKET_GROUP=1 select it.
-#ifndef RTW_PACKET
-#define RTW_PACKET 0  // world BVH walks
-#endif
-#ifndef RTW_PACKET_GROUP
-#define RTW_PACKET_GROUP 0  // group BVH walks from uniform roots
-#endif
-template <class LEAF>
-RTW_D void packet_walk(const scene& S, int root, const slab_ray& sr, float t0, int dneg, const hit_state& h,
-                       uint16_t* ws, LEAF&& leaf) {
-    int wsp = 0;  // wave-uniform
-    int ni = root;
-    for (;;) {
-        const bvh_node32 nd = node_s(S, ni);
-        const bool pass = slab32(nd, sr, t0, t_hi32(h.t));
-        const uint64_t m = __builtin_amdgcn_ballot_w64(pass);
-        if (m) {
-            if (nd.b < 0) {
-                if (pass) leaf(nd.a, -nd.b);
-            } else {
-                const int pad = nd.b >> 28, right = nd.b & 0x0fffffff;
-                const bool lf = (((dneg >> (pad & 3)) ^ (pad >> 2)) & 1) == 0;
-                const uint64_t ml = __builtin_amdgcn_ballot_w64(pass && lf);
-                const bool left_first = 2 * __builtin_popcountll(ml) >= __builtin_popcountll(m);
-                if (wsp < lds_stack::wave_cap)  // always true: depth checked at upload
-                    ws[wsp++] = (uint16_t)(left_first ? right : nd.a);
-                ni = left_first ? nd.a : right;
-                continue;
-            }
-        }
-        if (wsp == 0) break;
-        ni = __builtin_amdgcn_readfirstlane((int)ws[--wsp]);
-    }
-}
-
-// BVH over the prims of one group (items = prim indices).
-// PK: the root is wave-uniform and no walk encloses this one (the media
-// walk, the world runs): the packet walk (with LDS stacks).
-template <bool PK = false, class STK>
-RTW_D void group_bvh(const scene& S, int root, int root4, const ray& r, double t_min, hit_state& h, STK& stk,
-                     int base, bool movers) {
+// BVH over the prims of one group (items = prim indices).  (Packet walks of
+// a wave-uniform root, 4-wide nodes and fused walks of two group trees all
+// measured slower: DESIGN.md §4.2, §4.2b.)
+template <class STK>
+RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_state& h, STK& stk, int base,
+                     bool movers) {
     const double fc = motion_frac(S, r.t, movers);
     const slab_ray sr = make_slab_ray(S, r);
     const int dneg = dir_mask(r.d);
     const float t0 = t_lo32(t_min);
-    if constexpr (RTW_BVH4 && std::is_same<STK, lds_stack>::value) {
-        walk4(S, root4, sr, t0, h, stk, base, [&](int la, int lc) {
-            for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
-        });
-        return;
-    }
-    if constexpr (PK && RTW_PACKET_GROUP && std::is_same<STK, lds_stack>::value) {
-        packet_walk(S, root, sr, t0, dneg, h, stk.wave_row(), [&](int la, int lc) {
-            for (int k = 0; k < lc; ++k) arbitrate_item_u(S, ld(&S.items[la + k]), r, t_min, h, fc);
-        });
-        return;
-    }
     int sp = base;
-#ifndef RTW_GROUP_WW
-#define RTW_GROUP_WW 1
-#endif
-#if RTW_GROUP_WW
     stk.at(sp++) = root;
     // while-while, as in world_closest (+6.6 % Book 2 BVH, whose 1 000-sphere
     // cluster is a group BVH).  (The world walk's child-test form measured
     // -0.4 % here, C5.)
-#if RTW_SPEC_GROUP
-    // speculative (RTW_SPEC_WALK's reasoning): a lane holding its leaf keeps
-    // popping nodes while other lanes look for theirs; a second leaf it meets
-    // goes back on its stack for the next round
-    for (;;) {
-        int la = 0, lc = 0;
-        bool stall = false;  // met its second leaf: waits for the others
-        for (;;) {
-            if (__builtin_amdgcn_ballot_w64(lc == 0 && sp > base) == 0) break;
-            if (sp == base || stall) continue;
-            const int ni = stk.at(--sp);
-            const bvh_node32 nd = node_at(S, ni);
-            if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
-            const int c = node_count(nd);
-            if (c == 0) {
-                if (sp + 2 <= STK::cap) push_children(nd, dneg, stk, sp);
-            } else if (lc == 0) {
-                la = nd.a, lc = c;
-            } else {
-                stk.at(sp++) = ni;  // tested again when popped
-                stall = true;
-            }
-        }
-        if (__builtin_amdgcn_ballot_w64(lc != 0) == 0) break;
-        for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
-    }
-#elif RTW_GROUP_TOS
-    // top of stack in a register: an inner node's nearer child is the next
-    // node to visit, so it is kept in `next` instead of being pushed and
-    // popped again at once through the LDS stack (only the farther child is
-    // stored); the visiting order is unchanged
-    --sp;  // the root is `next`, not a stack entry
-    int next = root;
-    bool have = true;
-    for (;;) {
-        int la = 0, lc = 0;
-        while (lc == 0 && (have || sp > base)) {
-            const int ni = have ? next : stk.at(--sp);
-            have = false;
-            const bvh_node32 nd = node_at(S, ni);
-            if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
-            lc = node_count(nd);
-            la = nd.a;
-            if (lc == 0 && sp + 1 <= STK::cap) {  // always true: depth checked at upload
-                const int pad = nd.b >> 28, right = nd.b & 0x0fffffff;
-                const bool left_first = (((dneg >> (pad & 3)) ^ (pad >> 2)) & 1) == 0;
-                stk.at(sp++) = left_first ? right : nd.a;
-                next = left_first ? nd.a : right;
-                have = true;
-            }
-        }
-        if (lc == 0) break;
-        leaf_items(S, la, lc, r, t_min, h, fc);
-    }
-#else
     for (;;) {
         int la = 0, lc = 0;
         while (lc == 0 && sp > base) {
@@ -1987,87 +1222,13 @@ RTW_D void group_bvh(const scene& S, int root, int root4, const ray& r, double t
         if (lc == 0) break;
         leaf_items(S, la, lc, r, t_min, h, fc);
     }
-#endif
-#else
-    stk.at(sp++) = root;
-    while (sp > base) {
-        const bvh_node32 nd = node_at(S, stk.at(--sp));
-        if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
-        const int cnt = node_count(nd);
-        if (cnt > 0) {
-            for (int k = 0; k < cnt; ++k) arbitrate_item(S, S.items[nd.a + k], r, t_min, h, fc);
-        } else if (sp + 2 <= STK::cap) {  // always true: depth checked at upload
-            push_children(nd, dneg, stk, sp);
-        }
-    }
-#endif
-}
-
-// Two group BVHs of the media walk in one while-while loop.  Walked one
-// after the other, a wave pays the longest ground walk of its lanes and then
-// the longest cluster walk; here a lane whose first walk ends moves on to the
-// second while the others continue, so the wave pays roughly the longest
-// SUM (scripts/sim_walk.py: Book 2's group steps per wave-segment 51 -> 35).
-// e0 has no ops (the world frame) and is visited first; e1, visited later
-// in the list, is walked now from the closest hit of e0 on: with the larger
-// t_max it finds the closest of its items beyond which nothing it holds can
-// win later, so its result (hb), merged at its own visit by better() --
-// the rule every item test applies, order-independent -- is the list order's
-// (a deterministic group: no draws; its nodes are culled only against a t
-// that bounds what could still win).
-#ifndef RTW_FUSE_GROUPS
-#define RTW_FUSE_GROUPS 0
-#endif
-// (fuse false: e0's walk alone -- the media walk's one group-BVH walk site)
-template <class STK>
-RTW_D void fused_group_bvh(const scene& S, const entry_v& e0, const entry_v& e1, bool fuse, const ray& r,
-                           double t_min, hit_state& h, hit_state& hb, STK& stk) {
-    const float t0 = t_lo32(t_min);
-    slab_ray sr;
-    int dneg;
-    {
-        const ray r0 = entry_local_ray<true>(e0, r);
-        sr = make_slab_ray(S, r0);
-        dneg = dir_mask(r0.d);
-    }
-    double fc = motion_frac(S, r.t, e0.movers);
-    int sp = 0;
-    stk.at(sp++) = e0.bvh_root;
-    bool second = false;
-    hit_state hg = h;
-    for (;;) {
-        int la = 0, lc = 0;
-        while (lc == 0 && sp > 0) {  // group_bvh's inner loop, unchanged
-            const bvh_node32 nd = node_at(S, stk.at(--sp));
-            if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
-            lc = node_count(nd);
-            la = nd.a;
-            if (lc == 0 && sp + 2 <= STK::cap) push_children(nd, dneg, stk, sp);
-        }
-        if (lc == 0) {
-            if (second || !fuse) break;
-            second = true;  // e0 done: its winner bounds e1's walk
-            hg = h;
-            const ray r1 = entry_local_ray<true>(e1, r);
-            sr = make_slab_ray(S, r1);
-            dneg = dir_mask(r1.d);
-            fc = motion_frac(S, r.t, e1.movers);
-            stk.at(sp++) = e1.bvh_root;
-            continue;
-        }
-        leaf_items(S, la, lc, entry_local_ray<true>(second ? e1 : e0, r), t_min, h, fc);
-    }
-    if (!fuse) return;
-    hb = h;
-    if (h.prim == hg.prim) hb.prim = -1;  // e1 holds nothing that beats e0's winner
-    h = hg;
 }
 
 // (called with wave-uniform entries only: the media walk)
 template <int F, class STK>
 RTW_D void group_closest(const scene& S, const entry_v& e, const ray& r, double t_min, hit_state& h, STK& stk) {
     if ((F & F_GBVH) && e.bvh_root >= 0)
-        group_bvh<true>(S, e.bvh_root, e.bvh_root4, r, t_min, h, stk, 0, e.movers);
+        group_bvh(S, e.bvh_root, r, t_min, h, stk, 0, e.movers);
     else
         group_scan(S, e.first_prim, e.n_prims, r, t_min, h, e.movers);
 }
@@ -2088,9 +1249,6 @@ RTW_D bool boundary_t(const scene& S, const entry_v& e, const ray& r, double t0,
 // Both boundary probes of a one-sphere boundary from one quadratic.
 // Measured (1 MI355X, A/B, profiles/r04/ab_pin_quad_boxrcp.log): C5 slice
 // 656.1 vs 639.3 Msamples/s.
-#ifndef RTW_MEDIUM_ONE_QUADRATIC
-#define RTW_MEDIUM_ONE_QUADRATIC 1
-#endif
 // The boundary distances of constant_medium::hit (hittable.h:438-449): the
 // closest boundary hit t1 in (-DBL_MAX, DBL_MAX), then the closest beyond
 // t1 + 0.0001f; false when either probe misses.  `r` is the ray in the
@@ -2098,7 +1256,7 @@ RTW_D bool boundary_t(const scene& S, const entry_v& e, const ray& r, double t0,
 template <int F, class STK>
 RTW_D bool medium_bounds(const scene& S, const entry_v& e, const ray& r, int n_outer, double& t1, double& t2,
                          STK& stk) {
-    if (RTW_MEDIUM_ONE_QUADRATIC && e.n_prims == 1 && e.bvh_root < 0 && is_sphere(ld(&S.prims[e.first_prim].type))) {
+    if (e.n_prims == 1 && e.bvh_root < 0 && is_sphere(ld(&S.prims[e.first_prim].type))) {
         // A boundary that is one sphere (wave-uniform: the media walk's
         // entries are): both probes (hittable.h:438-449) are that sphere's
         // test on the same ray, so its quadratic is solved once and each
@@ -2139,29 +1297,11 @@ RTW_D bool medium_bounds(const scene& S, const entry_v& e, const ray& r, int n_o
 // hand it their moved ray, hittable.h:299-311, 373-404)
 template <int F, class STK>
 RTW_D bool medium_t(const scene& S, const entry_v& e, const ray& rw, double t_min, double t_max, uint32_t& rng,
-                    double& t_out, STK& stk, int visit = 0, volatile double* cache = nullptr) {
+                    double& t_out, STK& stk) {
     const int n_outer = rd<true>(&e.p->n_outer_ops);
     const ray r = ops_in<true>(e, rw, 0, n_outer);
     double t1, t2;
-#ifndef RTW_MEDIUM_CACHE  // measured -8 % on the C5 slice (ab_cache_leafrcp.log: its scratch array): off
-#define RTW_MEDIUM_CACHE 0
-#endif
-    // boundary cache (scene::media visits): a later visit of this medium on
-    // the same ray reads the distances its first visit found (NaN: no
-    // boundary hit); the slot is wave-uniform, the cache a per-lane scratch
-    // array (stored once, read once: cheaper than the probes it replaces)
-    const int slot = RTW_MEDIUM_CACHE && cache ? ((visit >> kVisitSlotShift) & 15) - 1 : -1;
-    if (slot >= 0 && (visit & kVisitReuse)) {
-        t1 = cache[2 * slot];
-        t2 = cache[2 * slot + 1];
-        if (!(t1 == t1)) return false;
-    } else if (!medium_bounds<F>(S, e, r, n_outer, t1, t2, stk)) {
-        if (slot >= 0) cache[2 * slot] = __builtin_nan("");
-        return false;
-    } else if (slot >= 0) {
-        cache[2 * slot] = t1;
-        cache[2 * slot + 1] = t2;
-    }
+    if (!medium_bounds<F>(S, e, r, n_outer, t1, t2, stk)) return false;
     if (t1 < t_min) t1 = t_min;
     if (t2 > t_max) t2 = t_max;
     if (t1 >= t2) return false;
@@ -2197,54 +1337,26 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
         int sp = 0;
         stk.at(sp++) = S.world_bvh_root;
         // Leaf items: prims (~prim) or entries (their groups, flat or BVH)
-#ifndef RTW_BVH_SHARE_A
-#define RTW_BVH_SHARE_A 1
-#endif
         const double a = dot(r.d, r.d);
-        const bool oka = RTW_BVH_SHARE_A && walk_ray_ok(S, r, fc) && div_hw_ok_b(a);
-        const double ya = RTW_BVH_SHARE_A ? rcp_hw(a) : 0.0;
+        const bool oka = walk_ray_ok(S, r, fc) && div_hw_ok_b(a);
+        const double ya = rcp_hw(a);
         auto leaf = [&](int la, int lc) {
             for (int k = 0; k < lc; ++k) {
                 const int it = S.items[la + k];
                 if (it < 0) {  // plain one-prim entry, its prim stored as ~prim by the upload
-                    if (RTW_BVH_SHARE_A)
-                        arbitrate_a(S, ~it, r, kTMin, h, fc, ya, oka);
-                    else
-                        arbitrate(S, ~it, r, kTMin, h, fc);
+                    arbitrate_a(S, ~it, r, kTMin, h, fc, ya, oka);
                     continue;
                 }
                 const entry_v e = view_entry<false>(S, it);
                 const ray lr = entry_local_ray<false>(e, r);
                 if ((F & F_GBVH) && e.bvh_root >= 0) {
-                    group_bvh(S, e.bvh_root, e.bvh_root4, lr, kTMin, h, stk, sp, S.mv_common != 0);
+                    group_bvh(S, e.bvh_root, lr, kTMin, h, stk, sp, S.mv_common != 0);
                 } else {
                     for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMin, h, fc);
                 }
             }
         };
-        if constexpr ((F & F_GBVH) == 0 && RTW_PACKET && std::is_same<STK, lds_stack>::value) {
-            // the packet walk (packet_walk); leaf items are prims (~prim) or
-            // entries, wave-uniform
-            packet_walk(S, S.world_bvh_root, sr, t0, dneg, h, stk.wave_row(), [&](int la, int lc) {
-                for (int k = 0; k < lc; ++k) {
-                    const int it = ld(&S.items[la + k]);
-                    if (it < 0) {  // plain one-prim entry
-                        arbitrate_u(S, ~it, r, kTMin, h, fc, ya, oka);
-                        continue;
-                    }
-                    const entry_v e = view_entry<true>(S, it);
-                    const ray lr = entry_local_ray<true>(e, r);
-                    for (int i = 0; i < e.n_prims; ++i)
-                        arbitrate_u(S, e.first_prim + i, lr, kTMin, h, fc, 0.0, false);  // exact quotients
-                }
-            });
-            return h;
-        }
-        if constexpr ((F & F_GBVH) == 0 && RTW_BVH4 && std::is_same<STK, lds_stack>::value) {
-            walk4(S, S.world_root4, sr, t0, h, stk, 0, leaf);
-            return h;
-        }
-        if constexpr ((F & F_GBVH) == 0 && RTW_CHILD_TEST) {
+        if constexpr ((F & F_GBVH) == 0) {
             // Children tested by their parent's iteration: expanding an inner
             // node loads both children and slab-tests them together; a lane
             // continues with the nearer child that passes and stacks the
@@ -2261,7 +1373,6 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             sp = 0;
             for (;;) {
                 int la = 0, lc = 0;  // this lane's pending leaf: first item, count
-#if RTW_SPEC_WALK
                 // speculative while-while: a lane that holds its leaf keeps
                 // walking (with the closest t it has) while other lanes of the
                 // wave still look for theirs, and stops at its next leaf,
@@ -2283,45 +1394,6 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                 }
                 if (__builtin_amdgcn_ballot_w64(lc != 0) == 0) break;
                 if (lc != 0) leaf(la, lc);
-#else
-                while (lc == 0) {
-                    if (!have) {
-                        if (sp == 0) break;
-                        const bvh_node32 nd = node_at(S, stk.at(--sp));
-                        if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
-                        ca = nd.a, cb = nd.b, have = true;
-                    }
-                    if (cb < 0) {  // a leaf
-                        la = ca, lc = -cb, have = false;
-                        break;
-                    }
-                    have = expand_children(S, sr, t0, t_hi32(h.t), dneg, stk, sp, ca, cb);
-                }
-                if (lc == 0) break;
-                leaf(la, lc);
-#endif
-            }
-        } else if constexpr ((F & F_GBVH) == 0) {
-            // while-while: each lane walks inner nodes until it reaches a
-            // leaf that passes its slab test (or its stack runs dry), then
-            // all lanes test their leaves together, so the leaf code runs
-            // once per leaf round instead of in every node iteration that
-            // holds any leaf lane.  Every lane visits the same nodes and
-            // leaves in the same order as one node per iteration would.
-            // (+2 % random_balls BVH; Book 2, whose leaves start nested
-            // group walks, loses 2.6 % and keeps the form below.)
-            for (;;) {
-                int la = 0, lc = 0;  // this lane's pending leaf: first item, count
-                while (lc == 0 && sp > 0) {
-                    const bvh_node32 nd = node_at(S, stk.at(--sp));
-                    if (!slab32(nd, sr, t0, t_hi32(h.t))) continue;
-                    lc = node_count(nd);
-                    la = nd.a;
-                    if (lc == 0 && sp + 2 <= STK::cap)  // always true: depth checked at upload
-                        push_children(nd, dneg, stk, sp);
-                }
-                if (lc == 0) break;
-                leaf(la, lc);
             }
         } else {
             while (sp > 0) {
@@ -2345,37 +1417,20 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
             const bool pw = (rng & 63) == 0;  // a sample of the walks
             uint64_t pw_t = pw ? clock64() : 0;
 #endif
-#if RTW_MEDIUM_CACHE
-            volatile double cache[2 * kMediumSlots];  // medium boundary distances by slot (scratch)
-#else
-            volatile double* const cache = nullptr;
-#endif
-            hit_state hb{in_place<kDblMaxBits>(), -1, false};  // the fused walk's result for fuse_entry
             for (int k = 0; k < S.n_media; ++k) {
                 const int visit = ld(&S.media[k]);
                 const int ei = visit & kVisitEntry;
                 const entry_v e = view_entry<true>(S, ei);
-                if (RTW_FUSE_GROUPS && (F & F_GBVH) && e.kind != RTW_ENTRY_MEDIUM && e.bvh_root >= 0 &&
-                    !(visit & kVisitMerge)) {
-                    // every group-BVH walk of the media walk, fused or not, at one site
-                    const bool fuse = (visit & kVisitFuse) != 0;
-                    fused_group_bvh(S, e, view_entry<true>(S, fuse ? S.fuse_entry : ei), fuse, r, kTMin, h, hb,
-                                    stk);
-                } else if (RTW_FUSE_GROUPS && (F & F_GBVH) && (visit & kVisitMerge)) {
-                    if (hb.prim != -1 && better(hb.t, hb.prim, hb.rect, h.t, h.prim, h.rect, h.prim != -1)) h = hb;
-                } else if (e.kind == RTW_ENTRY_MEDIUM) {
+                if (e.kind == RTW_ENTRY_MEDIUM) {
                     double t;
-                    if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk, visit, cache)) {
+                    if (medium_t<F>(S, e, r, kTMin, h.t, rng, t, stk)) {
                         h.t = t;
                         h.prim = -(2 + ei);
                         h.rect = false;
                     }
                 } else {
                     const ray lr = entry_local_ray<true>(e, r);
-                    if (RTW_FUSE_GROUPS && (F & F_GBVH))  // group BVHs took the branch above
-                        group_scan(S, e.first_prim, e.n_prims, lr, kTMin, h, e.movers);
-                    else
-                        group_closest<F>(S, e, lr, kTMin, h, stk);
+                    group_closest<F>(S, e, lr, kTMin, h, stk);
                 }
 #ifdef RTW_PROF_WALK
                 if (pw) {
@@ -2399,7 +1454,7 @@ RTW_D hit_state world_closest(const scene& S, const ray& r, uint32_t& rng, STK& 
                     const entry_v e = view_entry<true>(S, ei);
                     lr = entry_local_ray<true>(e, r);
                     if ((F & F_GBVH) && e.bvh_root >= 0) {
-                        group_bvh<true>(S, e.bvh_root, e.bvh_root4, lr, kTMin, h, stk, 0, e.movers);
+                        group_bvh(S, e.bvh_root, lr, kTMin, h, stk, 0, e.movers);
                         continue;
                     }
                 }
@@ -2512,22 +1567,56 @@ RTW_D d3 texture_value(const scene& S, int id, d3 p) {
 template <bool STATIC>
 RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
     if (L.kind == RTW_LIGHT_XZ_RECT) {  // hittable.h:208-222
+        // xz_rect::hit (hittable.h:184-200, validate: an XZ light is an xz
+        // rect) without its early returns: t, a, b and the pdf are formed for
+        // every lane and a miss selects 0 -- one branch level less of
+        // exec-mask bookkeeping per light per bounce (the world walk's rects
+        // likewise, rect_axis_rcp<BL>); a missing lane's values are never
+        // used.  Measured T +0.27 % (profiles/r05/ab_r5w_light_rect_branchless.log).
         const rtw_prim& q = S.prims[L.prim];
-        const ray r{o, v, kFltMax};
-        double t;
-        if (!rect_t(q, r, 0.001, __builtin_inf(), t)) return 0;
+        const double t = (q.p[4] - o.y) / v.y;
+        const double a = o.x + t * v.x;
+        const double b = o.z + t * v.z;
+        const bool hit = !(t < 0.001 || t > __builtin_inf()) && !(a < q.p[0] || a > q.p[1] || b < q.p[2] || b > q.p[3]);
         const double area = (q.p[1] - q.p[0]) * (q.p[3] - q.p[2]);
         const double distance_squared = t * t * len2(v);
 #if RTW_RADIANCE_FAST
-        // |dot(v, n)| / |v| folded into one quotient (v.y != 0: the rect was hit)
-        return rad_div(distance_squared * len(v), fabs(v.y) * area);
+        // |dot(v, n)| / |v| folded into one quotient (v.y != 0 where the rect
+        // was hit; a missing lane divides by 1, so rad_div's wave vote is
+        // the hitting lanes' as before)
+        const double pdf = rad_div(distance_squared * len(v), hit ? fabs(v.y) * area : 1.0);
 #else
         const double cosine = fabs(dot(v, d3{0, 1, 0}) / len(v));
-        return distance_squared / (cosine * area);
+        const double pdf = distance_squared / (cosine * area);
 #endif
+        return hit ? pdf : 0.0;
     }
     if (L.kind == RTW_LIGHT_SPHERE) {  // sphere.h:88-99
         const rtw_prim& q = S.prims[L.prim];
+#if RTW_AB_LSPH
+        {
+            // sphere::hit (sphere.h:46-81) without its early returns: both
+            // roots and the pdf formed for every lane, a miss selects 0
+            const d3 oc = o - (STATIC ? ld3(q.p) : sphere_center(q, kFltMax, motion_frac(S, kFltMax, q.type >= DP_MOVING_COMMON)));
+            const double a = dot(v, v);
+            const double b = dot(oc, v);
+            const double c = dot(oc, oc) - q.p[9];
+            const double disc = b * b - a * c;
+            const bool pos = disc > 0;
+            const double sq = RTW_SQRT(pos ? disc : 1.0);
+            const double r0 = (-b - sq) / a, r1 = (-b + sq) / a;
+            const bool hit = pos && ((r0 < __builtin_inf() && r0 > 0.001) || (r1 < __builtin_inf() && r1 > 0.001));
+#if RTW_RADIANCE_FAST
+            const double cos_theta_max = RTW_SQRT(1 - q.p[9] / len2(ld3(q.p) - o));
+            const double pdf = rad_div(1.0, hit ? kTwoPi * (1.0 - cos_theta_max) : 1.0);
+#else
+            const double cos_theta_max = RTW_SQRT(1 - q.p[9] / len2(ld3(q.p) - o));  // p[9] = radius * radius
+            const double solid_angle = kTwoPi * (1.0 - cos_theta_max);
+            const double pdf = 1.0 / solid_angle;
+#endif
+            return hit ? pdf : 0.0;
+        }
+#endif
         const ray r{o, v, kFltMax};
         double t;
         // (STATIC: no moving spheres, the fraction is never read)
@@ -2646,25 +1735,17 @@ RTW_D double schlick_r0(double cosine, double r0) { return r0 + (1 - r0) * pow5(
 
 // ------------------------------------------------------------------ camera
 // camera::get_ray camera.h:36-50, random_in_unit_disk :61-69 (y drawn first)
-// (RTW_DISK_FP32: the rejection loop decided in fp32 as random_in_unit_sphere's)
-#ifndef RTW_DISK_FP32
-#define RTW_DISK_FP32 RTW_RIUS_FP32
-#endif
-// RTW_PIN_RAYGEN: a pinhole camera (lens_radius 0, no zero origin
-// coordinate) draws the disk point only to advance the engine: rd = 0 * p is
-// a signed zero, so origin + offset == origin, and (x - origin) - offset ==
+// (the rejection loop decided in fp32 as random_in_unit_sphere's)
+// A pinhole camera (`pin`, the host's camera_is_pinhole: lens_radius 0, no
+// zero origin coordinate, finite u and v) draws the disk point only to
+// advance the engine: rd = 0 * p is a signed zero, so is the offset
+// u * rd.x + v * rd.y, so origin + offset == origin, and (x - origin) - offset ==
 // x - origin (that difference is never -0: x - origin is exactly zero only
 // for x == origin != 0, which rounds to +0) -- the point is not formed and
 // the offset not computed.  The draws, the time and the ray are the
 // reference's (camera.h:36-50).
-#ifndef RTW_PIN_RAYGEN
-#define RTW_PIN_RAYGEN 1
-#endif
-RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng) {
-    d3 p;
-    const bool pin = RTW_PIN_RAYGEN && c.lens_radius == 0.0 && c.origin[0] != 0.0 && c.origin[1] != 0.0 &&
-                     c.origin[2] != 0.0;  // wave-uniform: the camera is
-#if RTW_DISK_FP32
+RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng, bool pin) {
+    d3 p;  // (pin is wave-uniform: the job's)
     {
         constexpr float k2Rf = (float)(2.0 / kCanonR);
         auto lead = [&](uint32_t raw) { return __builtin_fmaf((float)(raw - 1u), k2Rf, -1.0f); };
@@ -2674,7 +1755,6 @@ RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng
             return d3{x, y, 0} * 2.0 - d3{1, 1, 0};
         };
         uint32_t y1, y2, x1, x2;
-#if RTW_RNG_JUMP
         // draws 1..4 of a try from s0: y2, x2 by two-step jumps, y1 = a s0 and
         // x1 = a y2 only where the point is formed (never for a pinhole)
         uint32_t s0;
@@ -2694,27 +1774,7 @@ RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng
             y1 = mr_jump(s0, kMrA), x1 = mr_jump(y2, kMrA);
             p = exact(y1, y2, x1, x2);
         }
-#else
-        for (;;) {
-            y1 = mr_next(rng), y2 = mr_next(rng);
-            x1 = mr_next(rng), x2 = mr_next(rng);
-            const float px = lead(x2), py = lead(y2);
-            const float d32 = __builtin_fmaf(px, px, py * py);
-            if (d32 < 1.0f - 0x1p-14f) break;
-            if (!(d32 < 1.0f + 0x1p-14f)) continue;
-            const d3 q = exact(y1, y2, x1, x2);
-            if (dot(q, q) < 1.0) break;
-        }
-        if (!pin) p = exact(y1, y2, x1, x2);
-#endif
     }
-#else
-    do {
-        const double y = rnd01(rng);
-        const double x = rnd01(rng);
-        p = d3{x, y, 0} * 2.0 - d3{1, 1, 0};
-    } while (dot(p, p) >= 1.0);
-#endif
     if (pin) {
         const double time = c.time0 + rnd01(rng) * (c.time1 - c.time0);
         const d3 dir = ld3(c.lower_left) + ld3(c.horizontal) * s + ld3(c.vertical) * t - ld3(c.origin);

@@ -21,6 +21,7 @@
 // draw uses it.)
 #pragma once
 
+#include <cassert>
 #if defined(__HIPCC__)
 #define RTW_HD __host__ __device__ __forceinline__
 #else
@@ -80,6 +81,7 @@ struct udiv32 {
     uint32_t m, s1, s2;
 };
 inline udiv32 udiv_magic(uint32_t d) {  // host, d >= 1
+    assert(d >= 1 && "udiv_magic: divisor 0");  // callers pass validated sizes (npix, nx, S_pass)
     uint32_t l = 0;
     while (l < 32 && (1ull << l) < d) ++l;
     const uint64_t m = (((1ull << 32) * ((1ull << l) - d)) / d) + 1;

@@ -116,7 +116,6 @@ struct fscene {
     // nodes of the BFS numbering, set by the kernel; 0 elsewhere)
     const rtwd::node_store* lnodes;
     int32_t n_lnodes;
-    float node_scale;  // RTW_NODE16: rtwd::scene::node_scale
 };
 
 // uniform (scalar) loads of a prim's fields
@@ -345,11 +344,7 @@ RTW_D slab_rayf make_slab(const fscene& S, const fray& r) {
     slab_rayf s;
     s.inv = f3{rcp(r.d.x), rcp(r.d.y), rcp(r.d.z)};
     s.oi = f3{-r.o.x * s.inv.x, -r.o.y * s.inv.y, -r.o.z * s.inv.z};
-#if RTW_NODE16
-    s.inv = s.inv * S.node_scale;  // the nodes' fp16 bounds are coordinates / node_scale
-#else
     (void)S;
-#endif
     return s;
 }
 RTW_D bool slab(const bvh_node32& nd, const slab_rayf& s, float t0, float t1) {
@@ -364,7 +359,7 @@ RTW_D bool slab(const bvh_node32& nd, const slab_rayf& s, float t0, float t1) {
 }
 // (explicit address spaces, as rtwd::node_at: an LDS read for packet nodes,
 // a global read for the rest)
-// PALL: the all-in-packet shortcut (RTW_PACKET_ALL) is compiled in; the
+// PALL: the all-in-packet shortcut is compiled in; the
 // media kernel leaves it out (its packet never holds every node at two
 // workgroups per CU, and the branch cost it a spilled register: C5 fp32
 // -1.4 %, profiles/r05/ab_r5f_fpall.log)
@@ -373,16 +368,8 @@ RTW_D bvh_node32 node_at(const fscene& S, int i) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     using lds_v4 = const __attribute__((address_space(3))) v4u;
     using glb_v4 = const __attribute__((address_space(1))) v4u;
-#if RTW_NODE16
-    v4u a;
-    if (i < S.n_lnodes)
-        a = *(lds_v4*)(S.lnodes + i);
-    else
-        a = *(glb_v4*)(S.nodes + i);
-    return rtwd::decode16(a.x, a.y, a.z, a.w);
-#else
     v4u a, b;
-    if (PALL && RTW_PACKET_ALL && S.n_lnodes >= S.n_nodes) {  // every node in the packet: wave-uniform
+    if (PALL && S.n_lnodes >= S.n_nodes) {  // every node in the packet: wave-uniform
         lds_v4* p = (lds_v4*)(S.lnodes + i);
         a = p[0], b = p[1];
     } else if (i < S.n_lnodes) {
@@ -397,41 +384,25 @@ RTW_D bvh_node32 node_at(const fscene& S, int i) {
     __builtin_memcpy(&nd, &a, 16);
     __builtin_memcpy(reinterpret_cast<char*>(&nd) + 16, &b, 16);
     return nd;
-#endif
 }
 
-// Speculative while-while for the fp32 world walk (RTW_SPEC_WALK's form
-// without the child test): measured C3 fp32 4 142 vs 4 703 Msamples/s (1
-// MI355X, A/B, profiles/r03/ab_fp32_spec_rejected.log; the 8-wave kernel
-// spills more around the two-level loop).  Off.
-#ifndef RTW_FAST_SPEC
-#define RTW_FAST_SPEC 0
-#endif
+// (The speculative while-while of the fp64 world walk, without its child
+// test, measured C3 fp32 -12 % here: the 8-wave kernel spills more around
+// the two-level loop.)
 // Workgroup size of k_fast: the LDS node packet is one per workgroup, so
 // larger workgroups at the same waves per CU share a larger packet (as
 // rtwd::kPBlock for k_persist); 1 024 threads = two workgroups of 16 waves
 // per CU at 8 waves per SIMD (rtw_kernels.hip RTW_FAST_BVH_WAVES: measured).
-#ifndef RTW_FAST_BLOCK
-#define RTW_FAST_BLOCK 1024
-#endif
-constexpr int kFastBlock = RTW_FAST_BLOCK;
-// ... and of the media kernel (F_MEDIA: Book 2), with its waves per SIMD
-// (rtw_kernels.hip RTW_FAST_MEDIA_WAVES).  Measured (1 MI355X, A/B,
+constexpr int kFastBlock = 1024;
+// ... and of the media kernel (F_MEDIA: Book 2).  Measured (1 MI355X, A/B,
 // profiles/r05/ab_r5e_fmedia.log, C5 fp32 slice): 1 024 threads at 8 waves
 // (64 VGPRs, 17 spilled) 843; 896 at 7 (72 VGPRs, 9 spilled, a 1 632-node
 // packet) 472; 768 at 6 (spill-free, every node in the packet, its fetch
 // shortcut) 751.  1 024 stays.
-#ifndef RTW_FAST_MEDIA_BLOCK
-#define RTW_FAST_MEDIA_BLOCK 1024
-#endif
-constexpr int fast_block(int F) { return (F & rtwd::F_MEDIA) ? RTW_FAST_MEDIA_BLOCK : kFastBlock; }
-// the all-in-packet node fetch (node_at<PALL>): compiled into the media
-// kernel only with RTW_FAST_MEDIA_PALL (its packet holds every node only at
-// smaller workgroups)
-#ifndef RTW_FAST_MEDIA_PALL
-#define RTW_FAST_MEDIA_PALL 0
-#endif
-constexpr bool fast_pall(int F) { return (F & rtwd::F_MEDIA) == 0 || RTW_FAST_MEDIA_PALL; }
+constexpr int fast_block(int F) { return kFastBlock; }
+// the all-in-packet node fetch (node_at<PALL>): not in the media kernel (its
+// packet holds every node only at smaller workgroups)
+constexpr bool fast_pall(int F) { return (F & rtwd::F_MEDIA) == 0; }
 
 // traversal stacks: a column of 16-bit node ids per lane in LDS (column
 // stride: the workgroup size), or a private array
@@ -453,25 +424,6 @@ RTW_D void group_bvh(const fscene& S, int root, const fray& r, float tmin, fhit&
     const slab_rayf sr = make_slab(S, r);
     const float t0 = tmin > 0 ? tmin * 0.5f : tmin * 2.0f - 1e-6f;
     int sp = base;
-#if RTW_GROUP_TOS
-    // the next node (the left child of the node just expanded) in a
-    // register, only the right one through the stack: the order is unchanged
-    int next = root;
-    bool have = true;
-    while (have || sp > base) {
-        const int ni = have ? next : stk.at(--sp);
-        have = false;
-        const bvh_node32 nd = node_at<PALL>(S, ni);
-        if (!slab(nd, sr, t0, h.t)) continue;
-        if (nd.b < 0) {
-            for (int k = 0; k < -nd.b; ++k) arbitrate_item(S, S.items[nd.a + k], r, tmin, h);
-        } else if (sp + 1 <= STK::cap) {
-            stk.at(sp++) = nd.b & 0x0fffffff;
-            next = nd.a;
-            have = true;
-        }
-    }
-#else
     stk.at(sp++) = root;
     while (sp > base) {
         const bvh_node32 nd = node_at<PALL>(S, stk.at(--sp));
@@ -483,7 +435,6 @@ RTW_D void group_bvh(const fscene& S, int root, const fray& r, float tmin, fhit&
             stk.at(sp++) = nd.a;
         }
     }
-#endif
 }
 
 template <int F, class STK>
@@ -531,59 +482,6 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
         const float t0 = kTMinF * 0.5f;
         int sp = 0;
         stk.at(sp++) = S.world_bvh_root;
-#if RTW_FAST_SPEC
-        // speculative while-while (rtwd::RTW_SPEC_WALK): lanes walk inner
-        // nodes until every lane holds a leaf or is out of nodes; a lane that
-        // meets a second leaf puts it back and waits; then the leaves are
-        // tested together
-        for (;;) {
-            int la = 0, lc = 0;
-            bool stall = false;
-            for (;;) {
-                if (__builtin_amdgcn_ballot_w64(lc == 0 && sp > 0) == 0) break;
-                if (sp == 0 || stall) continue;
-                const int ni = stk.at(--sp);
-                const bvh_node32 nd = node_at<fast_pall(F)>(S, ni);
-                if (!slab(nd, sr, t0, h.t)) continue;
-                if (nd.b >= 0) {
-                    if (sp + 2 <= STK::cap) stk.at(sp++) = nd.b & 0x0fffffff, stk.at(sp++) = nd.a;
-                } else if (lc == 0) {
-                    la = nd.a, lc = -nd.b;
-                } else {
-                    stk.at(sp++) = ni;  // tested again when popped
-                    stall = true;
-                }
-            }
-            if (__builtin_amdgcn_ballot_w64(lc != 0) == 0) break;
-            for (int k = 0; k < lc; ++k) {
-                const int it = S.items[la + k];
-                if (it < 0) {  // a plain one-prim entry: ~prim
-                    arbitrate(S, ~it, r, kTMinF, h);
-                    continue;
-                }
-                const ent_v e = view_entry<false>(S, it);
-                const fray lr = ops_in<false>(e, r, 0, e.n_ops);
-                if ((F & rtwd::F_GBVH) && e.bvh_root >= 0)
-                    group_bvh<fast_pall(F)>(S, e.bvh_root, lr, kTMinF, h, stk, sp);
-                else
-                    for (int i = 0; i < e.n_prims; ++i) arbitrate(S, e.first_prim + i, lr, kTMinF, h);
-            }
-        }
-        if (false)
-#endif
-#if RTW_GROUP_TOS
-        // the next node in a register (group_bvh's form): the root, then the
-        // left child of each node expanded; only right children are stacked
-        for (int next = (sp = 0, S.world_bvh_root), have = 1; have || sp > 0;) {
-            const int ni = have ? next : stk.at(--sp);
-            have = 0;
-            const bvh_node32 nd = node_at<fast_pall(F)>(S, ni);
-            if (!slab(nd, sr, t0, h.t)) continue;
-            if (nd.b >= 0) {
-                if (sp + 1 <= STK::cap) stk.at(sp++) = nd.b & 0x0fffffff, next = nd.a, have = 1;
-                continue;
-            }
-#else
         while (sp > 0) {
             const bvh_node32 nd = node_at<fast_pall(F)>(S, stk.at(--sp));
             if (!slab(nd, sr, t0, h.t)) continue;
@@ -591,7 +489,6 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 if (sp + 2 <= STK::cap) stk.at(sp++) = nd.b & 0x0fffffff, stk.at(sp++) = nd.a;
                 continue;
             }
-#endif
             for (int k = 0; k < -nd.b; ++k) {
                 const int it = S.items[nd.a + k];
                 if (it < 0) {  // a plain one-prim entry: ~prim
@@ -908,15 +805,9 @@ RTW_D seg_f shade(const fscene& S, const fray& r, const fhit& h, uint32_t& rng, 
 }
 
 // the material class of a hit, the key the regrouping kernel sorts by
-// (the sorted block's order, as k_persist_sort's RTW_KEY_ORDER: material
-// order, path-ending keys last, unless RTW_KEY_ORDER selects another)
-#if defined(RTW_KEY_ORDER) && RTW_KEY_ORDER == 1
-enum { FK_LAMB = 0, FK_EMIT, FK_DIEL, FK_MISS, FK_METAL, FK_ISO, FK_IDLE, FK_N };
-#elif RTW_KEY_ORDER == 2
-enum { FK_LAMB = 0, FK_EMIT, FK_MISS, FK_DIEL, FK_METAL, FK_ISO, FK_IDLE, FK_N };
-#else
+// (the sorted block's order, as k_persist_sort's: material order,
+// path-ending keys last)
 enum { FK_LAMB = 0, FK_DIEL, FK_METAL, FK_ISO, FK_EMIT, FK_MISS, FK_IDLE, FK_N };
-#endif
 RTW_D int hit_key(const fscene& S, const fhit& h) {
     if (h.prim == -1) return FK_MISS;
     const int mat = h.prim <= -2 ? S.entries[-h.prim - 2].phase_material : S.prims[h.prim].material;

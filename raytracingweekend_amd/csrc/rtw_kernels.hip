@@ -103,6 +103,7 @@ struct job_t {
     uint32_t npix;       // pixels of this call (n_rows * nx)
     int32_t nx, ny, row_begin, row_step, s_begin, max_depth;
     uint32_t spp_pass;   // samples per pixel in this pass
+    uint32_t cam_pin;    // camera_is_pinhole(camera): camera_ray's pinhole shortcut applies
     rtwd::udiv32 div_npix, div_nx, div_spp;  // magic numbers of npix, nx, spp_pass (sample_coords)
     double* L;           // per-sample radiance, L[3q + c] (pass-local sample id q)
 #if RTW_STRICT_RADIANCE
@@ -115,49 +116,24 @@ struct job_t {
 
 // Pass-local sample ids are sample-major: q = sample * npix + pixel, so a
 // wave's 64 consecutive ids are 64 neighbouring pixels and k_reduce reads
-// each sample plane coalesced.  RTW_PIXEL_MAJOR=1 makes them pixel-major
-// (q = pixel * spp_pass + sample): a wave's 64 radiance records then fill
-// whole lines of one contiguous 1.5 KB run instead of partial sectors of 64
-// pixels' planes (1.55x the record bytes), but k_reduce has to stage each
-// pixel's run through LDS to sum it in sample order.  Measured on T (1
-// MI355X, rocprofv3): traversal kernel 148.99 vs 149.12 ms, k_reduce 3.75 vs
-// 2.66 ms, the whole step -0.5 % (profiles/r03/ab_pixel_major.log) -- so
-// sample-major stays.  Results do not depend on it: the RNG is keyed by
-// (pixel, sample) and each pixel's records are summed in sample order.
-#ifndef RTW_PIXEL_MAJOR
-#define RTW_PIXEL_MAJOR 0
-#endif
+// each sample plane coalesced.  (Pixel-major ids fill whole lines with a
+// wave's records but make k_reduce stage each pixel's run through LDS: the
+// step -0.5 %, profiles/r03/ab_pixel_major.log.)  Results do not depend on
+// the order: the RNG is keyed by (pixel, sample) and each pixel's records are
+// summed in sample order.
 
-// A sample's radiance record.  RTW_NT_RECORDS: non-temporal stores -- the
-// records are read back only by k_reduce after the launch, so they stream
-// past the L2 instead of evicting the lines the traversal reuses (scene,
-// nodes beyond the LDS packet, spill slots).
-// Measured (1 MI355X, A/B, profiles/r05/ab_r5b_*.log): T 4 463 vs 4 465,
-// C5 slice 663.7 vs 663.3 -- the records cost the L2 nothing measurable.  Off.
-#ifndef RTW_NT_RECORDS
-#define RTW_NT_RECORDS 0
-#endif
+// A sample's radiance record.  (Non-temporal stores measured +-0 on T and
+// C5, profiles/r05/ab_r5b_*.log.)
 template <typename T>
 __device__ __forceinline__ void store_record(T* o, T x, T y, T z) {
-#if RTW_NT_RECORDS
-    __builtin_nontemporal_store(x, o);
-    __builtin_nontemporal_store(y, o + 1);
-    __builtin_nontemporal_store(z, o + 2);
-#else
     o[0] = x, o[1] = y, o[2] = z;
-#endif
 }
 
 // pass-local sample id -> pixel (i, j) and global sample index s
 __device__ __forceinline__ void sample_coords(const job_t& J, uint32_t q, int& i, int& j, int& s) {
 // (the quotients by exact magic-number division, rtw_div.h udiv_fast)
-#if RTW_PIXEL_MAJOR
-    const uint32_t rem = udiv_fast(q, J.div_spp);
-    const uint32_t sl = q - rem * J.spp_pass;
-#else
     const uint32_t sl = udiv_fast(q, J.div_npix);
     const uint32_t rem = q - sl * J.npix;
-#endif
     const uint32_t k = udiv_fast(rem, J.div_nx);
     i = (int)(rem - k * (uint32_t)J.nx);
     j = J.row_begin + (int)k * J.row_step;
@@ -201,7 +177,7 @@ __device__ __forceinline__ ray camera_sample(const job_t& J, uint32_t q, uint32_
     c.time0 = ld(&cp->time0);
     c.time1 = ld(&cp->time1);
     c.lens_radius = ld(&cp->lens_radius);
-    return camera_ray(c, u, v, rng);
+    return camera_ray(c, u, v, rng, J.cam_pin != 0);
 }
 
 __device__ __forceinline__ void raygen(const job_t& J, const fresh_t& F, uint32_t k, uint32_t q) {
@@ -395,7 +371,7 @@ struct path_st {
 // Outcome of one segment: the path continues with throughput *= f and the
 // next call's ray, or ends with radiance thr * E, or ends with radiance 0.
 enum { SEG_CONTINUE = 0, SEG_END = 1, SEG_END_ZERO = 2 };
-constexpr uint32_t kDepthBits = 0x3fffffffu;  // a path's depth below RTW_SORT_MIXTURE's choice bits
+constexpr uint32_t kDepthBits = 0x3fffffffu;  // a path's depth (bits above: reserved, zero)
 
 // A sink receives the outcome inside the shading branch that produced it:
 //   cont(f, next)   the path continues (throughput *= f, ray `next`)
@@ -456,12 +432,7 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
                                           prof_t& pf) {
     const ray r = x.r;
     uint32_t rng = x.rng;
-#if RTW_SORT_MIXTURE
-    const uint32_t depth = x.depth & kDepthBits;
-    const uint32_t mix = x.depth >> 30;  // 0: not drawn yet; 1 cosine, 2 lights (k_persist_sort)
-#else
     const uint32_t depth = x.depth;
-#endif
     // the scattered branches' common tail: the next color() call has depth
     // depth - 1, and returns 0 when that is 0
     auto scatter = [&](const d3& f, const d3& p, const d3& dir) -> int {
@@ -533,11 +504,7 @@ __device__ __forceinline__ int shade_core(const scene& S, path_st& x, double t, 
         d3 dir;
         double pdf_val, cosine;
         if (LIGHTS || (!NOLIGHTS && S.n_lights > 0)) {  // mixture_pdf(cosine_pdf, hittable_pdf(lights)) pdf.h:55-79
-#if RTW_SORT_MIXTURE
-            dir = mixture_generate(S, sf, p, rng, mix);
-#else
             dir = mixture_generate(S, sf, p, rng);
-#endif
             pf.mark(PS_SAMPLE);
             // both cosines before the light pdfs, so the normal and the frame
             // are dead while those run (the values are what the reference
@@ -737,12 +704,9 @@ __global__ __launch_bounds__(kBlock) RTW_SEG_ATTR void k_segment(scene S, job_t 
 // dry), every lane generates one ray into the wave's LDS buffer, and idle
 // lanes pop rays from that buffer.  A wave exits when the queue is exhausted,
 // its buffer is empty and its last path has ended.
-// Camera samples a wave generates at once into its batch: 64 (lane-full
-// ray generation) unless RTW_PBATCH(F) says fewer for that kernel -- a
-// smaller batch leaves LDS for parked origins and the node packet.
-#ifndef RTW_PBATCH
-#define RTW_PBATCH(F) 64
-#endif
+// Camera samples a wave generates at once into its batch: 64, lane-full ray
+// generation.
+constexpr int kPBatch = 64;
 // PIN (F_PIN): the origins are the camera's, read from the camera where a
 // sample is popped instead of stored per entry -- 24 B x 64 per wave less LDS
 // (24 KB per 1 024-thread workgroup), which the BVH node packet takes.
@@ -760,14 +724,14 @@ __device__ __forceinline__ d3 camera_origin(const job_t& J) {
     asm volatile("" : "+s"(cp));
     return d3{ld(&cp->origin[0]), ld(&cp->origin[1]), ld(&cp->origin[2])};
 }
-// F_PIN applies to a render whose camera makes every ray at its origin
-// (-DRTW_PIN_KERNELS=0: never, for A/B)
-#ifndef RTW_PIN_KERNELS
-#define RTW_PIN_KERNELS 1
-#endif
+// F_PIN applies to a render whose camera makes every ray at its origin: no
+// lens, no zero origin coordinate, and finite u, v (a non-finite u or v --
+// vup parallel to the view direction makes u = unit_vector(0) = NaN -- gives
+// the reference a NaN offset and NaN rays, camera.h:36-50)
 inline bool camera_is_pinhole(const rtw_camera_desc& c) {
-    return RTW_PIN_KERNELS && c.lens_radius == 0.0 && c.origin[0] != 0.0 && c.origin[1] != 0.0 &&
-           c.origin[2] != 0.0;
+    bool uv = true;
+    for (int k = 0; k < 3; ++k) uv = uv && std::isfinite(c.u[k]) && std::isfinite(c.v[k]);
+    return c.lens_radius == 0.0 && c.origin[0] != 0.0 && c.origin[1] != 0.0 && c.origin[2] != 0.0 && uv;
 }
 
 // Occupancy: left alone the compiler gives k_persist 160-230 VGPRs (2-3
@@ -808,55 +772,18 @@ __device__ __forceinline__ const persist_args& args_now() {
 }
 
 // LST: BVH traversal stacks in LDS (one column per lane) instead of scratch.
-//
-// DIRECT (RTW_PERSIST_DIRECT): the heavy kernels (media scenes: ~10 000 VALU
-// instructions per wave-segment, where a camera ray is ~1 %) take camera
-// samples straight into the idle lanes -- no per-wave batch -- and spend the
-// batch's 16 KB of LDS on a slot per lane holding the path's ray between
-// iterations: read before traversal, read again before shading (so it is not
-// live in registers across the walk), and the continuation written there.
-// In registers that loop-carried ray was what the Book-2 kernel spilled to
-// scratch (9 VGPRs, 48 bytes per lane, most of its HBM write traffic).
-// BIN (RTW_BIN_RAYS): wave-level binning of rays by direction octant before
-// each world-BVH walk (A/B for the divergent random_balls BVH walks).
-#ifndef RTW_BIN_RAYS
-#define RTW_BIN_RAYS(F) 0
-#endif
-// Measured (1 MI355X, A/B): C5 slice 577 vs 617 Msamples/s, C3 2617 vs
-// 2711 -- the lane-partial camera sampling costs more than the spills it
-// removes, so it is off (-DRTW_PERSIST_DIRECT(F)=1 selects it).
-#ifndef RTW_PERSIST_DIRECT
-#define RTW_PERSIST_DIRECT(F) 0
-#endif
-// PARK (RTW_PARK_ORIGIN): the batch-fed form with each lane's ray ORIGIN kept
-// in an LDS slot between iterations (written where the ray is taken or
-// continued, read before the walk and again before shading), so it is not a
-// register value live across the walk: what the media kernel spilled to
-// scratch was three doubles of the loop-carried ray.
-// Measured (1 MI355X, A/B, profiles/r03/ab_park_rejected.log): with the
-// 64-entry batch the parked origins take 24 KB from the node packet (C5 slice
-// 607.8 vs 623.3 Msamples/s); with 32-entry batches (RTW_PBATCH 32, half-lane
-// ray generation) the C5 kernel is spill-free (ScratchSize 0, 0 VGPR spills)
-// and its LDS 8 KB smaller, but measures 615.9 vs 623.3 (C5) and 2 609 vs
-// 2 783 (C3): the three spilled doubles (stored once per iteration, reloaded
-// at the shading sites) cost less than either.  Off.
-#ifndef RTW_PARK_ORIGIN
-#define RTW_PARK_ORIGIN(F) 0
-#endif
+// The loop-carried ray stays in registers: every form that parked it in LDS
+// (the whole ray with lane-direct camera samples, or its origin beside
+// smaller batches) took that LDS from the node packet or the batches and
+// measured slower than the spills it removed.
 template <int F, int M, bool LDS, bool LST = false>
 __global__ __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist(persist_args) {
-    constexpr bool DIRECT = RTW_PERSIST_DIRECT(F);
-    constexpr bool BIN = RTW_BIN_RAYS(F) && !DIRECT;
-    constexpr bool PARK = RTW_PARK_ORIGIN(F) && !DIRECT && !BIN;
-    constexpr int NB = DIRECT ? 1 : RTW_PBATCH(F);
+    constexpr int NB = kPBatch;
     constexpr bool PIN = (F & F_PIN) != 0;
-    static_assert(NB >= 1 && NB <= 64, "batch of one wave");
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
     __shared__ uint32_t s_cnt[kPWaves];
-    __shared__ ray_batch_t<NB, PIN> s_batch[DIRECT ? 1 : kPWaves];
-    // DIRECT: each lane's ray (o, d, time); PARK: its origin
-    __shared__ double s_ray[DIRECT ? 7 : (PARK ? 3 : 1)][kPBlock];
+    __shared__ ray_batch_t<NB, PIN> s_batch[kPWaves];
     __shared__ double s_thr[3][kPBlock];  // each lane's path throughput
     __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kPBlock];
     __shared__ uint32_t s_q[kPBlock];     // each lane's sample id
@@ -868,9 +795,9 @@ void k_persist(persist_args) {
     }
     if (LST) {  // the BVH node packet (the top levels of every tree)
         const persist_args& A = args_now();
-        const uint4* src = reinterpret_cast<const uint4*>(RTW_BVH4 ? (const void*)A.S.nodes4 : (const void*)A.S.nodes);
+        const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
         uint4* dst = reinterpret_cast<uint4*>(s_scene + A.lds_nodes_off);
-        constexpr uint32_t kNode16 = (uint32_t)((RTW_BVH4 ? sizeof(bvh_node4) : sizeof(node_store)) / 16);
+        constexpr uint32_t kNode16 = (uint32_t)(sizeof(node_store) / 16);
         for (uint32_t k = threadIdx.x; k < A.lds_nodes * kNode16; k += kPBlock) dst[k] = src[k];
     }
     if (LDS || LST) __syncthreads();
@@ -878,21 +805,10 @@ void k_persist(persist_args) {
     const int own = blockIdx.x % kQShards;
     path_st x;
     x.depth = 0;
-    uint32_t home = threadIdx.x;  // BIN: the LDS slot (sample id, throughput) of this lane's path
     bool open = true;      // wave-uniform: the queue may still hold samples
     uint32_t bl = 0, bh = 0;  // wave-uniform: unread batch entries [bl, bh)
     uint32_t segs = 0;
     prof_t pf;
-    // the lane's parked ray (DIRECT)
-    auto park = [&](uint32_t me, const ray& r) {
-        s_ray[0][me] = r.o.x, s_ray[1][me] = r.o.y, s_ray[2][me] = r.o.z;
-        s_ray[3][me] = r.d.x, s_ray[4][me] = r.d.y, s_ray[5][me] = r.d.z;
-        if (!(F & F_STATIC)) s_ray[6][me] = r.t;
-    };
-    auto unpark = [&](uint32_t me) {
-        return ray{d3{s_ray[0][me], s_ray[1][me], s_ray[2][me]}, d3{s_ray[3][me], s_ray[4][me], s_ray[5][me]},
-                   (F & F_STATIC) ? 0.0 : s_ray[6][me]};
-    };
     for (;;) {
         // lane-dependent LDS addresses (batch, throughput, sample id, stack
         // columns) are formed from an opaque copy of the thread index where
@@ -901,45 +817,7 @@ void k_persist(persist_args) {
         uint32_t tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         const uint32_t ln = tid & 63;
-        if constexpr (DIRECT) {
-            // idle lanes take new camera samples, one reservation per wave
-            const bool idle = x.depth == 0;
-            const unsigned long long m = __ballot(idle);
-            if (open && m) {
-                const persist_args& A = args_now();
-                const job_t& J = A.J;
-                ctrs_t* const C = A.C;
-                const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
-                uint32_t left = (uint32_t)__popcll(m), given = 0, q = 0;
-                bool got = false;
-                for (int a = 0; a < kQShards && left; ++a) {
-                    const int sh = (own + a) % kQShards;
-                    const unsigned long long lim = shard_limit(sh, J.total);
-                    unsigned long long b = ~0ull;
-                    if (ln == 0) {
-                        const bool dry = a > 0 && __hip_atomic_load(&C->qshard[sh].v, __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_AGENT) >= lim;
-                        if (!dry) b = atomicAdd(&C->qshard[sh].v, (unsigned long long)left);
-                    }
-                    b = __shfl(b, 0, 64);
-                    if (b == ~0ull || b >= lim) continue;
-                    const uint32_t ok = (uint32_t)min((unsigned long long)left, lim - b);
-                    if (idle && rank >= given && rank < given + ok) {
-                        q = (uint32_t)shard_sample(sh, b + (rank - given));
-                        got = true;
-                    }
-                    given += ok;
-                    left -= ok;
-                }
-                if (left) open = false;
-                if (got) {
-                    park(tid, camera_sample(J, q, x.rng));
-                    s_q[tid] = q;
-                    s_thr[0][tid] = 1.0, s_thr[1][tid] = 1.0, s_thr[2][tid] = 1.0;
-                    x.depth = (uint32_t)J.max_depth;
-                }
-            }
-        } else {
+        {
             // (the wave's batch too: formed once per kernel, its per-array
             // addresses were held in 15 VGPRs across the whole loop)
             ray_batch_t<NB, PIN>& B = s_batch[tid >> 6];
@@ -994,11 +872,9 @@ void k_persist(persist_args) {
                     const uint32_t k = bl + rank;
                     const d3 o = PIN ? camera_origin(args_now().J) : d3{B.ox[k], B.oy[k], B.oz[k]};
                     x.r = ray{o, d3{B.dx[k], B.dy[k], B.dz[k]}, B.tm[k]};
-                    if constexpr (PARK) s_ray[0][tid] = x.r.o.x, s_ray[1][tid] = x.r.o.y, s_ray[2][tid] = x.r.o.z;
                     x.rng = B.rng[k];
-                    const uint32_t hm = BIN ? home : tid;
-                    s_q[hm] = B.q[k];
-                    s_thr[0][hm] = 1.0, s_thr[1][hm] = 1.0, s_thr[2][hm] = 1.0;
+                    s_q[tid] = B.q[k];
+                    s_thr[0][tid] = 1.0, s_thr[1][tid] = 1.0, s_thr[2][tid] = 1.0;
                     x.depth = (uint32_t)args_now().J.max_depth;
                 }
                 bl += min((uint32_t)__popcll(m), avail);
@@ -1006,49 +882,14 @@ void k_persist(persist_args) {
             }
         }
         if (!__any(x.depth != 0)) break;
-        if constexpr (BIN) {
-            // wave-level binning of the paths by direction octant before the
-            // walk (live paths by octant, idle lanes last): a counting sort
-            // over ballots, then every lane's path state -- ray, engine,
-            // depth, home slot -- is pushed to the lane of its rank
-            // (ds_permute, no LDS allocation, no block barrier)
-            const int key = x.depth == 0 ? 8 : (x.r.d.x < 0 ? 1 : 0) | (x.r.d.y < 0 ? 2 : 0) | (x.r.d.z < 0 ? 4 : 0);
-            uint32_t dst = 0, before = 0;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                const unsigned long long m = __ballot(key == k);
-                if (key == k) dst = before + (uint32_t)__popcll(m & lanemask_lt());
-                before += (uint32_t)__popcll(m);
-            }
-            const int addr = (int)(dst * 4);
-            auto push32 = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)v); };
-            auto push64 = [&](double v) {
-                const uint64_t b = __builtin_bit_cast(uint64_t, v);
-                const uint64_t lo = push32((uint32_t)b), hi = push32((uint32_t)(b >> 32));
-                return __builtin_bit_cast(double, lo | (hi << 32));
-            };
-            x.r.o.x = push64(x.r.o.x), x.r.o.y = push64(x.r.o.y), x.r.o.z = push64(x.r.o.z);
-            x.r.d.x = push64(x.r.d.x), x.r.d.y = push64(x.r.d.y), x.r.d.z = push64(x.r.d.z);
-            if (!(F & F_STATIC)) x.r.t = push64(x.r.t);
-            x.rng = push32(x.rng);
-            x.depth = push32(x.depth);
-            home = push32(home);
-        }
         pf.mark(PS_LOAD);
         if (x.depth != 0) {
-            if constexpr (DIRECT) x.r = unpark(tid);
-            if constexpr (PARK) x.r.o = d3{s_ray[0][tid], s_ray[1][tid], s_ray[2][tid]};
             const persist_args& A = args_now();
             scene S = A.S;
             hit_state h;
             if constexpr (LST) {
-                if constexpr (RTW_BVH4) {
-                    S.lnodes4 = reinterpret_cast<const bvh_node4*>(s_scene + A.lds_nodes_off);
-                    S.n_lnodes4 = (int32_t)A.lds_nodes;
-                } else {
-                    S.lnodes = reinterpret_cast<const node_store*>(s_scene + A.lds_nodes_off);
-                    S.n_lnodes = (int32_t)A.lds_nodes;
-                }
+                S.lnodes = reinterpret_cast<const node_store*>(s_scene + A.lds_nodes_off);
+                S.n_lnodes = (int32_t)A.lds_nodes;
                 lds_stack stk{&s_stack[0][tid]};
                 h = world_closest<F>(S, x.r, x.rng, stk);
             } else {
@@ -1064,17 +905,7 @@ void k_persist(persist_args) {
                                                         : SS.prims[h.prim].material].type);
 #endif
             // the outcome is applied inside the branch that produced it
-            uint32_t me = BIN ? home : tid;
-            if constexpr (DIRECT) {
-                // the ray again from its slot: the copy the walk used is dead
-                // from here on (a fresh index keeps the compiler from reusing it)
-                asm volatile("" : "+v"(me)::"memory");
-                x.r = unpark(me);
-            }
-            if constexpr (PARK) {
-                asm volatile("" : "+v"(me)::"memory");
-                x.r.o = d3{s_ray[0][me], s_ray[1][me], s_ray[2][me]};
-            }
+            uint32_t me = tid;
             auto radiance = [&](const d3& L) {
                 double* o = A2.J.L + 3 * (size_t)s_q[me];
                 store_record(o, L.x, L.y, L.z);
@@ -1109,12 +940,7 @@ void k_persist(persist_args) {
             auto sk = make_sink(
                 [&](const d3& f, const ray& r) {
                     s_thr[0][me] *= f.x, s_thr[1][me] *= f.y, s_thr[2][me] *= f.z;
-                    if constexpr (DIRECT) {
-                        park(me, r);  // the continuation waits in the lane's slot
-                    } else {
-                        nr = r;
-                        if constexpr (PARK) s_ray[0][me] = r.o.x, s_ray[1][me] = r.o.y, s_ray[2][me] = r.o.z;
-                    }
+                    nr = r;
                 },
                 [&](const d3& E) { radiance(d3{s_thr[0][me], s_thr[1][me], s_thr[2][me]} * E); },
                 [&]() {
@@ -1126,7 +952,7 @@ void k_persist(persist_args) {
                                        (F & F_NOLIGHTS) != 0>(SS, x, h.t, h.prim, sk, pf);
             if (out != SEG_CONTINUE)
                 x.depth = 0;
-            else if constexpr (!DIRECT)
+            else
                 x.r = nr;
             pf.mark(PS_STORE);
         }
@@ -1151,46 +977,14 @@ void k_persist(persist_args) {
 // to the lane of their rank, so most waves run one branch.  Idle lanes end
 // up together at the top of the block: they take fresh camera samples
 // there, so ray generation also runs nearly lane-full.
-// The keys' order is the order of the sorted block.  A wave whose 64 slots
-// straddle two keys pays for both branches, which argues for the cheap keys
-// (emitter, miss: one radiance record) between the expensive ones
-// (RTW_KEY_ORDER 1: lambertian, emitter, dielectric, miss, ...; 2:
-// lambertian, emitter, miss, dielectric, ...).  Measured (1 MI355X, A/B,
-// profiles/r03/ab_key_order_rejected.log): T 3 961 (1) / 4 108 (2) vs 4 424
-// Msamples/s (0), T fp32 -8 %, C2 +0.6 %.  The paths that END (emitter,
-// miss) are the lanes that take camera samples next: in material order they
-// sit together at the block's top, beside the idle ones, and ray generation
-// runs lane-full in one or two waves; between the materials they are spread
-// over more waves.  0: material order, path-ending keys last.
-#ifndef RTW_KEY_ORDER
-#define RTW_KEY_ORDER 0
-#endif
-#if RTW_KEY_ORDER == 1
-enum { K_LAMB = 0, K_EMIT, K_DIEL, K_MISS, K_METAL, K_ISO, K_IDLE, K_N };
-#elif RTW_KEY_ORDER == 2
-enum { K_LAMB = 0, K_EMIT, K_MISS, K_DIEL, K_METAL, K_ISO, K_IDLE, K_N };
-#else
-enum { K_LAMB = 0, K_LAMBL, K_DIEL, K_METAL, K_ISO, K_EMIT, K_MISS, K_IDLE, K_N };
-#endif
-// MIXTURE (RTW_SORT_MIXTURE, scenes with lights): a lambertian hit's mixture
-// choice (pdf.h:67, the first number its shading draws) is drawn right after
-// traversal and sorted on -- cosine lobe (K_LAMB) apart from light sampling
-// (K_LAMBL) -- so a cosine wave skips the lights' branches.  The choice rides
-// in the depth's top bits to shade_core (the draw order is the reference's:
-// nothing is drawn between the hit and the choice).  Measured (1 MI355X,
-// A/B, profiles/r05/ab_r5h_sort_mixture_rejected.log): T 4 572 vs 4 616
-// Msamples/s (-1.0 %): the extra key splits the lambertian waves once more
-// and the light-sampling waves still run both light kinds.
-#ifndef RTW_SORT_MIXTURE
-#define RTW_SORT_MIXTURE 0
-#endif
-#if RTW_KEY_ORDER != 0
-enum { K_LAMBL = K_N + 1 };  // (never produced)
-#endif
+// The keys' order is the order of the sorted block: material order, the
+// path-ending keys (emitter, miss) last.  The paths that end are the lanes
+// that take camera samples next: they sit together at the block's top,
+// beside the idle ones, so ray generation runs lane-full in one or two waves.
+// (Cheap keys between the expensive ones measured T -7 %, and sorting
+// lambertian hits on their mixture choice T -1 %: DESIGN.md §4.2c.)
+enum { K_LAMB = 0, K_DIEL, K_METAL, K_ISO, K_EMIT, K_MISS, K_IDLE, K_N };
 
-#ifndef RTW_SORT_BLOCK
-#define RTW_SORT_BLOCK 256
-#endif
 // Ray generation threshold: a wave takes camera samples only when at least
 // this many of its lanes are idle.  After shading a few lambertian paths per
 // wave end (pdf <= 0, depth), and a wave would run a whole camera_sample
@@ -1203,9 +997,11 @@ enum { K_LAMBL = K_N + 1 };  // (never produced)
 #ifndef RTW_REFILL_MIN
 #define RTW_REFILL_MIN 8
 #endif
-constexpr int kSortBlock = RTW_SORT_BLOCK;  // paths regrouped together (one workgroup)
+// Paths regrouped together (one workgroup).  (128 or 512 measured T -15 % /
+// -13 %)
+constexpr int kSortBlock = 256;
 constexpr int kSortWaves = kSortBlock / 64;
-// DPP (RTW_SORT_DPP): the counting sort's block prefix from a key-major
+// The counting sort's block prefix from a key-major
 // count table s_kc[key][wave] (kKeySlots x 4; slots of keys the scene cannot
 // produce stay zero): lane k < 8 of every wave reads key k's four per-wave
 // counts in one 16-B LDS read and forms their total and the count in the
@@ -1213,13 +1009,8 @@ constexpr int kSortWaves = kSortBlock / 64;
 // (three DPP row shifts) adds the paths of every key before k; each lane
 // fetches its own key's base with one ds_bpermute.  The plain form has every
 // lane read all 4 x K_N counts and sum them under selects (~67 VALU per
-// wave-iteration on T).  The same destinations either way (bit-identical
-// images, profiles/r05/parity_r5l.log).  Measured (1 MI355X, A/B,
-// profiles/r05/ab_r5l_sort_dpp.log): T 4 709 vs 4 571 Msamples/s (+3.0 %),
-// T fp32 8 094 vs 7 724 (+4.8 %), C2 +1.0 %, C2 fp32 +0.9 %.
-#ifndef RTW_SORT_DPP
-#define RTW_SORT_DPP 1
-#endif
+// wave-iteration on T); measured T +3.0 %, T fp32 +4.8 %
+// (profiles/r05/ab_r5l_sort_dpp.log).
 constexpr int kKeySlots = 8;
 __device__ __forceinline__ uint32_t sort_base_dpp(const uint32_t (*s_kc)[4], uint32_t lane, uint32_t wave, int key,
                                                   int k_idle, uint32_t& idle_total) {
@@ -1234,56 +1025,27 @@ __device__ __forceinline__ uint32_t sort_base_dpp(const uint32_t (*s_kc)[4], uin
     idle_total = (uint32_t)__builtin_amdgcn_readlane((int)tot, k_idle);
     return (uint32_t)__builtin_amdgcn_ds_bpermute(key << 2, (int)base);
 }
-#if RTW_SORT_DPP
-static_assert(kSortWaves == 4 && K_N <= kKeySlots, "RTW_SORT_DPP: 256-thread sort blocks, at most 8 keys");
-#endif
-// HOME_RAY (RTW_SORT_HOME_RAY): a path's ray and sample id live in its home
-// slot beside its throughput, so the exchange moves only the record's home
-// index, hit (t, prim), engine and depth -- 5 values instead of 12 -- and the
-// lanes read the ray from the home slot where they trace or shade it.
-#ifndef RTW_SORT_HOME_RAY
-#define RTW_SORT_HOME_RAY 0
-#endif
+static_assert(kSortWaves == 4 && K_N <= kKeySlots, "sort_base_dpp: 256-thread sort blocks, at most 8 keys");
 template <int F, int M, bool LDS>
 __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist_sort(persist_args) {
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
-#if RTW_SORT_DPP
     __shared__ __attribute__((aligned(16))) uint32_t s_kc[kKeySlots][kSortWaves];  // per key, lanes per wave
     if (threadIdx.x < kKeySlots * kSortWaves) (&s_kc[0][0])[threadIdx.x] = 0u;  // (before the barrier below)
-#else
-    __shared__ uint32_t s_kc[kSortWaves][K_N];  // per wave, lanes per key
-#endif
     __shared__ uint32_t s_seg[kSortWaves];
-    constexpr bool HR = RTW_SORT_HOME_RAY != 0;
-    constexpr int kX = HR ? 1 : kSortBlock;  // exchange arrays HOME_RAY does without
-    // the exchange: one path per slot (SoA); HOME_RAY: the ray and sample id
-    // at the record's home instead (h_o, h_d, h_tm, h_q)
-    __shared__ double x_o[3][kX], x_d[3][kX], x_tm[kX], x_t[kSortBlock];
+    // the exchange: one path per slot (SoA)
+    __shared__ double x_o[3][kSortBlock], x_d[3][kSortBlock], x_tm[kSortBlock], x_t[kSortBlock];
     __shared__ int32_t x_prim[kSortBlock];
-    __shared__ uint32_t x_rng[kSortBlock], x_depth[kSortBlock], x_q[kX], x_home[kSortBlock];
-    constexpr int kH = HR ? kSortBlock : 1;
-    __shared__ double h_o[3][kH], h_d[3][kH], h_tm[(F & F_STATIC) ? 1 : kH];
-    __shared__ uint32_t h_q[kH];
-    // the record's ray / sample id in slot `s` (exchange slot, or home)
+    __shared__ uint32_t x_rng[kSortBlock], x_depth[kSortBlock], x_q[kSortBlock], x_home[kSortBlock];
+    // the record's ray in slot `s`
     auto ray_at = [&](uint32_t s) {
-        if constexpr (HR)
-            return ray{d3{h_o[0][s], h_o[1][s], h_o[2][s]}, d3{h_d[0][s], h_d[1][s], h_d[2][s]},
-                       (F & F_STATIC) ? 0.0 : h_tm[s]};
-        else
-            return ray{d3{x_o[0][s], x_o[1][s], x_o[2][s]}, d3{x_d[0][s], x_d[1][s], x_d[2][s]},
-                       (F & F_STATIC) ? 0.0 : x_tm[s]};
+        return ray{d3{x_o[0][s], x_o[1][s], x_o[2][s]}, d3{x_d[0][s], x_d[1][s], x_d[2][s]},
+                   (F & F_STATIC) ? 0.0 : x_tm[s]};
     };
     auto put_ray = [&](uint32_t s, const ray& r) {
-        if constexpr (HR) {
-            h_o[0][s] = r.o.x, h_o[1][s] = r.o.y, h_o[2][s] = r.o.z;
-            h_d[0][s] = r.d.x, h_d[1][s] = r.d.y, h_d[2][s] = r.d.z;
-            if constexpr (!(F & F_STATIC)) h_tm[s] = r.t;
-        } else {
-            x_o[0][s] = r.o.x, x_o[1][s] = r.o.y, x_o[2][s] = r.o.z;
-            x_d[0][s] = r.d.x, x_d[1][s] = r.d.y, x_d[2][s] = r.d.z;
-            if constexpr (!(F & F_STATIC)) x_tm[s] = r.t;
-        }
+        x_o[0][s] = r.o.x, x_o[1][s] = r.o.y, x_o[2][s] = r.o.z;
+        x_d[0][s] = r.d.x, x_d[1][s] = r.d.y, x_d[2][s] = r.d.z;
+        if constexpr (!(F & F_STATIC)) x_tm[s] = r.t;
     };
     // Path throughputs stay put: each path record (live or idle) owns one
     // home slot of s_thr and carries its index through the exchange, so the
@@ -1349,11 +1111,8 @@ void k_persist_sort(persist_args) {
                     const ray r = camera_sample(J, q, x.rng);
                     const uint32_t me = threadIdx.x;
                     const uint32_t home = x_home[me];
-                    put_ray(HR ? home : me, r);  // (F_STATIC: the time is never read)
-                    if constexpr (HR)
-                        h_q[home] = q;
-                    else
-                        x_q[me] = q;
+                    put_ray(me, r);  // (F_STATIC: the time is never read)
+                    x_q[me] = q;
                     x.depth = (uint32_t)J.max_depth;
                     s_thr[0][home] = 1.0, s_thr[1][home] = 1.0, s_thr[2][home] = 1.0;
                 }
@@ -1366,7 +1125,7 @@ void k_persist_sort(persist_args) {
         int key = K_IDLE;
         if (x.depth != 0) {
             const uint32_t me = threadIdx.x;
-            x.r = ray_at(HR ? x_home[me] : me);
+            x.r = ray_at(me);
             const persist_args& A = args_now();
             const scene SS = LDS ? lds_scene(A.S, A.base, s_scene) : A.S;
             const hit_state h = world_closest<F>(A.S, x.r, x.rng);
@@ -1383,71 +1142,40 @@ void k_persist_sort(persist_args) {
                       : ty == RTW_MAT_METAL ? K_METAL
                       : ty == RTW_MAT_ISOTROPIC ? K_ISO
                                                 : K_EMIT;
-#if RTW_SORT_MIXTURE
-                if constexpr ((F & F_LIGHTS) && !(F & F_BLACK))
-                    if (key == K_LAMB && SS.render_type != RTW_RENDER_NORMAL) {
-                        const bool cosine = rnd01(x.rng) < 0.5;
-                        key = cosine ? K_LAMB : K_LAMBL;
-                        x.depth |= (cosine ? 1u : 2u) << 30;
-                    }
-#endif
             }
         }
         pk.mark(PS_TRAVERSE);
         // 3. counting sort of the block's paths by key (the record's home and
         // sample id are read from the lane's own slot before the barrier that
         // precedes the exchange's writes)
-        const uint32_t my_home = x_home[threadIdx.x], my_q = HR ? 0u : x_q[threadIdx.x < kX ? threadIdx.x : 0];
+        const uint32_t my_home = x_home[threadIdx.x], my_q = x_q[threadIdx.x];
         uint32_t rank_in_wave = 0;
         // keys the scene's material set cannot produce are skipped (their
         // counts stay 0; keep s_kc's slots zero for the prefix below)
         constexpr auto key_used = [](int k) {
-            return !((k == K_METAL && !(M & SF_METAL)) || (k == K_ISO && !(M & SF_ISO)) ||
-                     (k == K_LAMBL && !(RTW_SORT_MIXTURE && (F & F_LIGHTS))));
+            return !((k == K_METAL && !(M & SF_METAL)) || (k == K_ISO && !(M & SF_ISO)));
         };
 #pragma unroll
         for (int k = 0; k < K_N; ++k) {
             if (!key_used(k)) continue;
             const unsigned long long m = __ballot(key == k);
             if (key == k) rank_in_wave = (uint32_t)__popcll(m & lanemask_lt());
-#if RTW_SORT_DPP
             if (lane == 0) s_kc[k][wave] = (uint32_t)__popcll(m);
-#else
-            if (lane == 0) s_kc[wave][k] = (uint32_t)__popcll(m);
-#endif
         }
         __syncthreads();
-#if RTW_SORT_DPP
         uint32_t idle_total;
         const uint32_t dst = rank_in_wave + sort_base_dpp(s_kc, lane, wave, key, K_IDLE, idle_total);
-#else
-        uint32_t dst = rank_in_wave, idle_total = 0;
-#pragma unroll
-        for (int k = 0; k < K_N; ++k) {
-            if (!key_used(k)) continue;
-            uint32_t tot = 0, before = 0;
-#pragma unroll
-            for (int w = 0; w < kSortWaves; ++w) {
-                const uint32_t c = s_kc[w][k];
-                tot += c;
-                before += (w < (int)wave) ? c : 0u;
-            }
-            if (k < key) dst += tot;
-            if (k == key) dst += before;
-            if (k == K_IDLE) idle_total = tot;
-        }
-#endif
         if (idle_total == kSortBlock) break;  // block-uniform: nothing left to trace or take
         pk.mark(PS_HIT);
         // 4. move every path to the slot of its rank (an idle record's ray
         // is garbage and stays behind)
-        if (!HR && x.depth != 0) put_ray(dst, x.r);
+        if (x.depth != 0) put_ray(dst, x.r);
         x_home[dst] = my_home;
         x_t[dst] = th;
         x_prim[dst] = hp;
         x_rng[dst] = x.rng;
         x_depth[dst] = x.depth;
-        if constexpr (!HR) x_q[dst] = my_q;
+        x_q[dst] = my_q;
         __syncthreads();
         // (opaque, so the exchange's per-lane LDS addresses are formed here
         // from one register, not hoisted out of the loop one per array)
@@ -1458,21 +1186,21 @@ void k_persist_sort(persist_args) {
         pk.mark(PS_SAMPLE);
         // 5. shading, now mostly one branch per wave
         if (x.depth != 0) {
-            x.r = ray_at(HR ? x_home[me] : me);
+            x.r = ray_at(me);
             const persist_args& A = args_now();
             const scene SS = LDS ? lds_scene(A.S, A.base, s_scene) : A.S;
             prof_t pf;
             // the outcome is applied inside the branch that produced it
             auto radiance = [&](const d3& L) {
-                double* o = A.J.L + 3 * (size_t)(HR ? h_q[x_home[me]] : x_q[me]);
+                double* o = A.J.L + 3 * (size_t)x_q[me];
                 store_record(o, L.x, L.y, L.z);
             };
             auto sk = make_sink(
                 [&](const d3& f, const ray& nr) {
                     const uint32_t home = x_home[me];
                     s_thr[0][home] *= f.x, s_thr[1][home] *= f.y, s_thr[2][home] *= f.z;
-                    // the continuation ray waits in the lane's own slot (HOME_RAY: the home's)
-                    put_ray(HR ? home : me, nr);
+                    // the continuation ray waits in the lane's own slot
+                    put_ray(me, nr);
                 },
                 [&](const d3& E) {
                     const uint32_t home = x_home[me];
@@ -1506,16 +1234,10 @@ void k_persist_sort(persist_args) {
 // wave).  Waves run independently (no block barrier in the loop), so a wave
 // leaves as soon as the queue is dry and its last path has ended.
 // The fast mode's per-sample radiance record: 12 B of fp32 (k_reduce<float>
-// sums it in double in sample order, as it sums fp64 records); 24 B of fp64
-// under RTW_PIXEL_MAJOR, whose staged reduce reads doubles only.
+// sums it in double in sample order, as it sums fp64 records).
 __device__ __forceinline__ void store_record_f32(double* L, uint32_t q, float x, float y, float z) {
-#if RTW_PIXEL_MAJOR
-    double* o = L + 3 * (size_t)q;
-    o[0] = (double)x, o[1] = (double)y, o[2] = (double)z;
-#else
     float* o = reinterpret_cast<float*>(L) + 3 * (size_t)q;
     store_record(o, x, y, z);
-#endif
 }
 
 struct fast_args {
@@ -1525,8 +1247,8 @@ struct fast_args {
     rtwf::cam32 cam;
     uint32_t lds_nodes;  // k_fast<.., LST>: BVH node packet (the top nodes) in dynamic LDS
     // k_fast_sort<.., LDS>: each fscene array's byte offset in the LDS copy of
-    // the shading prefix, ~0u for one outside it (host-computed: lds_fscene's
-    // two 64-bit range compares per pointer per use become one 32-bit test)
+    // the shading prefix, ~0u for one outside it (host-computed: a range test of
+    // every pointer at every use, two 64-bit compares, becomes one 32-bit test)
     uint32_t lds_off[9];
 };
 
@@ -1553,30 +1275,19 @@ constexpr int FF_NONOISE = 1 << 12;
 #ifndef RTW_FAST_BVH_WAVES
 #define RTW_FAST_BVH_WAVES 8
 #endif
-#ifndef RTW_FAST_MEDIA_WAVES
-#define RTW_FAST_MEDIA_WAVES RTW_FAST_BVH_WAVES
-#endif
-#define RTW_FAST_WAVES_OF(F) (((F) & F_MEDIA) ? RTW_FAST_MEDIA_WAVES : RTW_FAST_BVH_WAVES)
-// HOME (RTW_FAST_HOME(F)): the path's throughput and sample id wait in the
-// lane's LDS home slots instead of registers (k_persist's plan), and the
-// segments are counted per wave in a scalar register -- the loop-carried
-// values the media kernel (F_MEDIA) spilled to scratch at 8 waves / 64 VGPRs.
-#ifndef RTW_FAST_HOME
-#define RTW_FAST_HOME(F) 0
-#endif
+// The path -- ray, throughput, engine, depth, sample id -- is in registers.
+// (Throughput and sample id in LDS home slots halve the media kernel's spill
+// stores but take a third of its node packet: -1 %)
 template <int F, bool LST>
-__global__ __launch_bounds__(rtwf::fast_block(F)) __attribute__((amdgpu_waves_per_eu(RTW_FAST_WAVES_OF(F))))
+__global__ __launch_bounds__(rtwf::fast_block(F)) __attribute__((amdgpu_waves_per_eu(RTW_FAST_BVH_WAVES)))
 void k_fast(fast_args) {
     using namespace rtwf;
     constexpr bool NOISE = (F & FF_NONOISE) == 0;
-    constexpr bool HOME = RTW_FAST_HOME(F) != 0;
     constexpr int kFB = fast_block(F);
     constexpr int kFW = kFB / 64;
     extern __shared__ __attribute__((aligned(16))) char s_nodes[];
     __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kFB];
     __shared__ uint32_t s_cnt[kFW];
-    __shared__ float s_thr[HOME ? 3 : 1][HOME ? kFB : 1];
-    __shared__ uint32_t s_q[HOME ? kFB : 1];
     if (LST) {  // the BVH node packet (the top levels of every tree)
         const fast_args& A = fast_args_now();
         const uint4* src = reinterpret_cast<const uint4*>(A.S.nodes);
@@ -1590,13 +1301,8 @@ void k_fast(fast_args) {
     fray r{f3{0, 0, 0}, f3{0, 0, 1}, 0};
     f3 thr{1, 1, 1};
     uint32_t rng = 0, depth = 0, q = 0, segs = 0;
-    uint32_t wsegs = 0;  // HOME: the wave's segments (wave-uniform)
     bool open = true;  // wave-uniform: the queue may still hold samples
     for (;;) {
-        // (HOME: an opaque copy of the thread index forms the slot addresses
-        // where they are used, as in k_persist)
-        uint32_t tid = threadIdx.x;
-        if constexpr (HOME) asm volatile("" : "+v"(tid));
         // idle lanes take new camera samples (RayTracingWeekend.cpp:227-231)
         const bool idle = depth == 0;
         const unsigned long long m = __ballot(idle);
@@ -1633,13 +1339,8 @@ void k_fast(fast_args) {
                 const float u = ((float)i + u01(rng)) * rcp((float)A.J.nx);
                 const float v = ((float)j + u01(rng)) * rcp((float)A.J.ny);
                 r = camera_ray(A.cam, u, v, rng);
-                if constexpr (HOME) {
-                    s_thr[0][tid] = 1.0f, s_thr[1][tid] = 1.0f, s_thr[2][tid] = 1.0f;
-                    s_q[tid] = nq;
-                } else {
-                    thr = f3{1, 1, 1};
-                    q = nq;
-                }
+                thr = f3{1, 1, 1};
+                q = nq;
                 depth = (uint32_t)A.J.max_depth;
             }
         }
@@ -1657,48 +1358,25 @@ void k_fast(fast_args) {
             priv_stackf stk;
             h = world_closest<F>(fast_args_now().S, r, rng, stk);
         }
-        if constexpr (HOME)
-            wsegs += (uint32_t)__popcll(__ballot(true));
-        else
-            ++segs;
+        ++segs;
         // one segment of color() (RayTracingWeekend.cpp:52-159)
         const seg_f sg = shade<NOISE>(fast_args_now().S, r, h, rng, depth);
         bool end = !sg.cont;
         f3 L{0, 0, 0};
-        if constexpr (HOME) {
-            uint32_t me = threadIdx.x;
-            asm volatile("" : "+v"(me));
-            const f3 t{s_thr[0][me], s_thr[1][me], s_thr[2][me]};
-            if (sg.cont) {
-                const f3 n = t * sg.w;
-                s_thr[0][me] = n.x, s_thr[1][me] = n.y, s_thr[2][me] = n.z;
-                r = sg.next;
-                --depth;
-            } else {
-                L = t * sg.w;
-                store_record_f32(fast_args_now().J.L, s_q[me], L.x, L.y, L.z);
-                depth = 0;
-            }
+        if (sg.cont) {
+            thr = thr * sg.w;
+            r = sg.next;
+            --depth;
         } else {
-            if (sg.cont) {
-                thr = thr * sg.w;
-                r = sg.next;
-                --depth;
-            } else {
-                L = thr * sg.w;
-            }
-            if (end) {
-                store_record_f32(fast_args_now().J.L, q, L.x, L.y, L.z);
-                depth = 0;
-            }
+            L = thr * sg.w;
+        }
+        if (end) {
+            store_record_f32(fast_args_now().J.L, q, L.x, L.y, L.z);
+            depth = 0;
         }
     }
-    if constexpr (HOME) {
-        if (lane == 0) s_cnt[threadIdx.x >> 6] = wsegs;
-    } else {
-        for (int off = 32; off > 0; off >>= 1) segs += __shfl_down(segs, off, 64);
-        if (lane == 0) s_cnt[threadIdx.x >> 6] = segs;
-    }
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_down(segs, off, 64);
+    if (lane == 0) s_cnt[threadIdx.x >> 6] = segs;
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
@@ -1707,7 +1385,7 @@ void k_fast(fast_args) {
     }
 }
 
-// RTW_FAST_LDS_OFF: k_fast_sort re-points its scene with the host's offsets
+// k_fast_sort re-points its scene with the host's offsets
 // (fast_args::lds_off) instead of range-testing every pointer at every use --
 // two 64-bit compares, a subtract and selects per pointer, twice per
 // iteration, on the scalar unit, which the fp32 kernel's issue shares with
@@ -1716,9 +1394,6 @@ void k_fast(fast_args) {
 // T fp32 8 654 vs 8 075 Msamples/s (+7.2 %), T fp64 +-0.  (The same offsets
 // for k_persist_sort's lds_scene, whose rebase has no range test, added
 // SALU and VALU there: not used.)
-#ifndef RTW_FAST_LDS_OFF
-#define RTW_FAST_LDS_OFF 1
-#endif
 __device__ __forceinline__ rtwf::fscene lds_fscene_off(const rtwf::fscene& S, const uint32_t* off, const char* lds) {
     rtwf::fscene L = S;
     auto rb = [&](const void* p, uint32_t o) -> const void* { return o != ~0u ? (const void*)(lds + o) : p; };
@@ -1731,25 +1406,6 @@ __device__ __forceinline__ rtwf::fscene lds_fscene_off(const rtwf::fscene& S, co
     L.ranvec = (const float*)rb(S.ranvec, off[6]);
     L.perm = (const int32_t*)rb(S.perm, off[7]);
     L.frames = (const float*)rb(S.frames, off[8]);
-    return L;
-}
-// Re-point an fp32 scene's arrays into an LDS copy of its allocation.
-__device__ __forceinline__ rtwf::fscene lds_fscene(const rtwf::fscene& S, const char* base, uint32_t bytes,
-                                                   const char* lds) {
-    rtwf::fscene L = S;
-    auto rb = [&](const void* p) -> const void* {
-        const char* c = (const char*)p;
-        return (c && c >= base && c < base + bytes) ? (const void*)(lds + (c - base)) : p;
-    };
-    L.prims = (const rtwf::prim32*)rb(S.prims);
-    L.entries = (const rtwf::ent32*)rb(S.entries);
-    L.ops = (const rtwf::op32*)rb(S.ops);
-    L.materials = (const rtwf::mat32*)rb(S.materials);
-    L.textures = (const rtwf::tex32*)rb(S.textures);
-    L.lights = (const rtw_light*)rb(S.lights);
-    L.ranvec = (const float*)rb(S.ranvec);
-    L.perm = (const int32_t*)rb(S.perm);
-    L.frames = (const float*)rb(S.frames);
     return L;
 }
 
@@ -1769,13 +1425,9 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
     using namespace rtwf;
     constexpr bool NOISE = (F & FF_NONOISE) == 0;
     extern __shared__ __attribute__((aligned(16))) char s_scene[];
-#if RTW_SORT_DPP
-    static_assert(FK_N <= kKeySlots, "RTW_SORT_DPP: at most 8 keys");
+    static_assert(FK_N <= kKeySlots, "sort_base_dpp: at most 8 keys");
     __shared__ __attribute__((aligned(16))) uint32_t s_kc[kKeySlots][kSortWaves];  // per key, lanes per wave
     if (threadIdx.x < kKeySlots * kSortWaves) (&s_kc[0][0])[threadIdx.x] = 0u;  // (before the barrier below)
-#else
-    __shared__ uint32_t s_kc[kSortWaves][FK_N];
-#endif
     __shared__ uint32_t s_seg[kSortWaves];
     __shared__ float x_o[3][kSortBlock], x_d[3][kSortBlock], x_tm[kSortBlock], x_t[kSortBlock];
     __shared__ int32_t x_prim[kSortBlock];
@@ -1850,11 +1502,7 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
             h = world_closest<F>(fast_args_now().S, r, rng, stk);
             ++segs;
             const fast_args& A = fast_args_now();
-#if RTW_FAST_LDS_OFF
             key = hit_key(LDS ? lds_fscene_off(A.S, A.lds_off, s_scene) : A.S, h);
-#else
-            key = hit_key(LDS ? lds_fscene(A.S, base, bytes, s_scene) : A.S, h);
-#endif
         }
         // 3. counting sort of the block's paths by key
         const uint32_t my_home = x_home[me], my_q = x_q[me];
@@ -1863,32 +1511,11 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
         for (int k = 0; k < FK_N; ++k) {
             const unsigned long long m = __ballot(key == k);
             if (key == k) rank_in_wave = (uint32_t)__popcll(m & lanemask_lt());
-#if RTW_SORT_DPP
             if (lane == 0) s_kc[k][wave] = (uint32_t)__popcll(m);
-#else
-            if (lane == 0) s_kc[wave][k] = (uint32_t)__popcll(m);
-#endif
         }
         __syncthreads();
-#if RTW_SORT_DPP
         uint32_t idle_total;
         const uint32_t dst = rank_in_wave + sort_base_dpp(s_kc, lane, wave, key, FK_IDLE, idle_total);
-#else
-        uint32_t dst = rank_in_wave, idle_total = 0;
-#pragma unroll
-        for (int k = 0; k < FK_N; ++k) {
-            uint32_t tot = 0, before = 0;
-#pragma unroll
-            for (int w = 0; w < kSortWaves; ++w) {
-                const uint32_t c = s_kc[w][k];
-                tot += c;
-                before += (w < (int)wave) ? c : 0u;
-            }
-            if (k < key) dst += tot;
-            if (k == key) dst += before;
-            if (k == FK_IDLE) idle_total = tot;
-        }
-#endif
         if (idle_total == kSortBlock) break;  // block-uniform: nothing left to trace or take
         // 4. move every path to the slot of its rank
         if (depth != 0) {
@@ -1910,11 +1537,7 @@ void k_fast_sort(fast_args, const char* base, uint32_t bytes) {
             const fray rr{f3{x_o[0][me], x_o[1][me], x_o[2][me]}, f3{x_d[0][me], x_d[1][me], x_d[2][me]}, x_tm[me]};
             const fhit hh{x_t[me], x_prim[me], false};
             const fast_args& A = fast_args_now();
-#if RTW_FAST_LDS_OFF
             const seg_f sg = shade<NOISE>(LDS ? lds_fscene_off(A.S, A.lds_off, s_scene) : A.S, rr, hh, rng, depth);
-#else
-            const seg_f sg = shade<NOISE>(LDS ? lds_fscene(A.S, base, bytes, s_scene) : A.S, rr, hh, rng, depth);
-#endif
             const uint32_t home = x_home[me];
             const f3 thr{s_thr[0][home], s_thr[1][home], s_thr[2][home]};
             if (sg.cont) {
@@ -2072,49 +1695,6 @@ __global__ void k_commit(ctrs_t* C) {
 }
 
 // running[pix] += sample s of pix for s = 0..S-1 in order (RayTracingWeekend.cpp:235-239)
-#if RTW_PIXEL_MAJOR
-// Pixel-major records: a block takes 64 consecutive pixels, whose records
-// are one contiguous run, and streams it through LDS in chunks of kRedChunk
-// samples (coalesced loads of each pixel's contiguous 24 * kRedChunk bytes);
-// thread 3k + c then adds channel c of pixel k's chunk in sample order.
-constexpr uint32_t kRedPix = 64, kRedChunk = 16;
-__global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ L, uint32_t npix, uint32_t spp,
-                                                   double* __restrict__ run) {
-    // one pixel's chunk per row, rows padded to an odd number of doubles so
-    // the summing threads' reads (3 per pixel, one row apart) spread over
-    // the LDS banks
-    constexpr uint32_t kRow = 3 * kRedChunk + 1;
-    __shared__ double s_rec[kRedPix * kRow];  // 24.5 KB
-    for (uint32_t p0 = blockIdx.x * kRedPix; p0 < npix; p0 += gridDim.x * kRedPix) {
-        const uint32_t np = min(kRedPix, npix - p0);
-        const uint32_t me = threadIdx.x;
-        const bool summer = me < 3 * np;
-        double acc = summer ? run[3 * (size_t)p0 + me] : 0.0;
-        for (uint32_t s0 = 0; s0 < spp; s0 += kRedChunk) {
-            const uint32_t cs = min(kRedChunk, spp - s0), row = 3 * cs;
-            __syncthreads();  // the previous chunk has been summed
-            if (cs == kRedChunk && np == kRedPix) {  // full chunk: constant shapes
-#pragma unroll
-                for (uint32_t k = me; k < kRedPix * 3 * kRedChunk; k += kBlock) {
-                    const uint32_t pk = k / (3 * kRedChunk), o = k - pk * (3 * kRedChunk);
-                    s_rec[pk * kRow + o] = L[3 * ((size_t)(p0 + pk) * spp + s0) + o];
-                }
-            } else {
-                for (uint32_t k = me; k < np * row; k += kBlock) {
-                    const uint32_t pk = k / row, o = k - pk * row;
-                    s_rec[pk * kRow + o] = L[3 * ((size_t)(p0 + pk) * spp + s0) + o];
-                }
-            }
-            __syncthreads();
-            if (summer) {
-                const uint32_t pk = me / 3, c = me - 3 * pk;
-                for (uint32_t s = 0; s < cs; ++s) acc = acc + s_rec[pk * kRow + 3 * s + c];
-            }
-        }
-        if (summer) run[3 * (size_t)p0 + me] = acc;
-    }
-}
-#else
 // Records are doubles (fp64 mode) or floats (the fp32 fast mode's radiance
 // is single precision: 12 B records, converted exactly to double here and
 // summed in the same order, so its sums are unchanged).
@@ -2132,14 +1712,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const T* __restrict__ L, uint
         run[3 * p] = r, run[3 * p + 1] = g, run[3 * p + 2] = bl;
     }
 }
-#endif
 // k_reduce's grid for npix pixels
 unsigned reduce_grid(uint64_t npix) {
-#if RTW_PIXEL_MAJOR
-    return (unsigned)std::min<uint64_t>((npix + kRedPix - 1) / kRedPix, 8192);
-#else
     return (unsigned)std::min<uint64_t>((npix + kBlock - 1) / kBlock, 4096);
-#endif
 }
 
 // accum[(j*nx+i)*3+c] += run[(k*nx+i)*3+c], j = row_begin + k*row_step
@@ -2230,7 +1805,6 @@ struct handle_t {
     int grid = 2048;
     int cus = 256;
     int stack_need = 0;  // deepest BVH stack a traversal of this scene can use
-    int stack4_need = INT32_MAX;  // ... with 4-wide walks (INT32_MAX: no 4-wide BVH)
     // BVH boxes of moving spheres cover the desc camera's shutter only
     bool bvh_motion = false;
     double shutter0 = 0.0, shutter1 = 0.0;
@@ -2289,28 +1863,6 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             for (int e = 0; e < d->n_entries; ++e) media.push_back(e);
             for (int e = 0; e < d->n_entries; ++e)
                 if (d->entries[e].kind == RTW_ENTRY_MEDIUM) media.push_back(e);
-        }
-        // boundary cache slots (rtw_device.h media_visit): a medium visited
-        // again later in the walk (the reference's second list walk) reuses
-        // the boundary distances its first visit found on the same ray; the
-        // first kMediumSlots media visited twice get a slot
-        // (RTW_MEDIUM_CACHE builds only: the default walk reads no slot, so
-        // its visits carry the bare entry index)
-        std::map<int, int> slot_of, seen;
-        for (int32_t e : media)
-            if (RTW_MEDIUM_CACHE && d->entries[e].kind == RTW_ENTRY_MEDIUM) ++seen[e];
-        for (int32_t& v : media) {
-            const int e = v;
-            if (d->entries[e].kind != RTW_ENTRY_MEDIUM || seen[e] < 2) continue;
-            auto it = slot_of.find(e);
-            if (it == slot_of.end()) {
-                if ((int)slot_of.size() >= kMediumSlots) continue;
-                const int slot = (int)slot_of.size();
-                slot_of[e] = slot;
-                v = e | ((slot + 1) << kVisitSlotShift);  // first visit: fills the slot
-            } else {
-                v = e | ((it->second + 1) << kVisitSlotShift) | kVisitReuse;  // later visit: reads it
-            }
         }
     }
     struct part {
@@ -2419,30 +1971,12 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         for (int i = R.first_prim; i < R.first_prim + R.n_prims; ++i)
             if (dprims[i].type == RTW_PRIM_SPHERE) dprims[i].p[5] = 0.0;
     }
-    // rect pairs of plain runs (rtw_device.h rect_pair_rcp): consecutive
-    // rects of one type with the same bounds in different planes
-    if (RTW_RECT_PAIRS) {
-        for (const world_run& R : runs) {
-            if (R.entry != WORLD_RUN_PLAIN) continue;
-            for (int i = R.first_prim; i + 1 < R.first_prim + R.n_prims; ++i) {
-                rtw_prim& a = dprims[i];
-                const rtw_prim& b = dprims[i + 1];
-                const bool rect = a.type >= RTW_PRIM_RECT_XY && a.type <= RTW_PRIM_RECT_YZ;
-                if (!rect || b.type != a.type || a.p[4] == b.p[4]) continue;
-                bool same = true;
-                for (int k = 0; k < 4; ++k) same = same && a.p[k] == b.p[k];
-                if (!same) continue;
-                a.flip |= kRectPairHead;
-                ++i;  // b is the pair's second rect
-            }
-        }
-    }
     // ysphere_scan's fp32 prefilter records (rtw_device.h): spheres of
     // y-sphere runs whose centre (incl. motion) is within 2^8 and radius
     // within 2^4 are filtered, others (the random_balls ground, r = 1000)
     // carry r^2 = +inf and always take the fp64 test; the maxima over the
     // filtered ones bound the prefilter's rounding error
-    // (RTW_YS_PACK: the records of a run are interleaved pairwise, spheres
+    // (the records of a run are interleaved pairwise, spheres
     // first + 2p and first + 2p + 1 sharing the 16 floats at 8 (first + 2p),
     // component c of member s at 2c + s; the last sphere of a run of odd
     // length keeps the plain record {cx, cy, cz, dy, rr} in its own 8 floats,
@@ -2459,15 +1993,10 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         if (R.entry != WORLD_RUN_YSPHERES) continue;
         for (int i = R.first_prim; i < R.first_prim + R.n_prims; ++i) {
             const rtw_prim& q = dprims[i];
-#if RTW_YS_PACK
             const int k = i - R.first_prim;
             const bool lone = k == R.n_prims - 1 && (k & 1) == 0;
             float* const rec = ysph.data() + 8 * (size_t)(R.first_prim + (k & ~1)) + (k & 1);
             auto f = [rec, lone](int c) -> float& { return rec[lone ? c : 2 * c]; };
-#else
-            float* const rec = ysph.data() + 8 * (size_t)i;
-            auto f = [rec](int c) -> float& { return rec[c]; };
-#endif
             const double dy = q.type == DP_MOVING_COMMON_Y ? q.p[5] : 0.0;
             f(0) = (float)q.p[0], f(1) = (float)q.p[1], f(2) = (float)q.p[2], f(3) = (float)dy;
             const bool small = std::fabs(q.p[0]) <= 256 && std::fabs(q.p[1]) <= 256 && std::fabs(dy) <= 256 &&
@@ -2576,175 +2105,6 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         for (rtw_entry& E : dentries)
             if (E.bvh_root >= 0) E.bvh_root = newid[E.bvh_root];
     }
-    // 4-wide BVHs (rtw_device.h bvh_node4, walk4) collapsed from the binary
-    // device trees: a node4's slots are the binary node's children, the
-    // inner slot with the largest surface area opened again (replaced in
-    // place by its two children) until there are four or only leaves are
-    // left.  Numbered breadth-first from all roots together (the LDS packet
-    // takes the first ones); leaves become leaf4 records (first item | count
-    // << 24).  A binary root that is a leaf gets a node4 of one slot.
-    std::vector<bvh_node4> n4;
-    std::vector<int32_t> leaf4;
-    std::vector<int> root4_of(dnodes32.size(), -1);  // binary root -> node4
-    int world_root4 = -1, depth4_world = 0, depth4_group = 0;
-    bool bvh4_ok = RTW_BVH4 && bvh_ok && !dnodes32.empty();
-    if (bvh4_ok) {
-        auto is_leaf = [&](int b) { return dnodes32[b].b < 0; };
-        auto area = [&](int b) {
-            const bvh_node32& N = dnodes32[b];
-            const double x = (double)N.hi[0] - N.lo[0], y = (double)N.hi[1] - N.lo[1], z = (double)N.hi[2] - N.lo[2];
-            return x * y + y * z + z * x;
-        };
-        std::vector<std::pair<int, int>> q;  // (binary node, depth4) in BFS order; node4 id = position
-        auto add_root = [&](int b) {
-            if (b < 0) return -1;
-            if (root4_of[b] >= 0) return root4_of[b];
-            root4_of[b] = (int)q.size();
-            q.push_back({b, 1});
-            return root4_of[b];
-        };
-        world_root4 = add_root(world_root);
-        for (const rtw_entry& E : dentries) add_root(E.bvh_root);
-        n4.reserve(dnodes32.size());
-        for (size_t qi = 0; qi < q.size(); ++qi) {
-            const int b = q[qi].first, dep = q[qi].second;
-            std::vector<int> slots;
-            if (is_leaf(b)) {
-                slots.push_back(b);
-            } else {
-                slots = {dnodes32[b].a, dnodes32[b].b & 0x0fffffff};
-                while (slots.size() < 4) {
-                    int pick = -1;
-                    double best = -1.0;
-                    for (size_t k = 0; k < slots.size(); ++k)
-                        if (!is_leaf(slots[k]) && area(slots[k]) > best) best = area(slots[k]), pick = (int)k;
-                    if (pick < 0) break;
-                    const bvh_node32& N = dnodes32[slots[pick]];
-                    slots[pick] = N.a;
-                    slots.insert(slots.begin() + pick + 1, N.b & 0x0fffffff);
-                }
-            }
-            bvh_node4 M;
-            std::memset(&M, 0, sizeof M);
-            for (int c = 0; c < 4; ++c) {
-                if (c >= (int)slots.size()) {  // unused slot: never passes (slab4)
-                    M.child[c] = kNoChild;
-                    continue;
-                }
-                const bvh_node32& N = dnodes32[slots[c]];
-                for (int k = 0; k < 3; ++k) M.lo[k][c] = N.lo[k], M.hi[k][c] = N.hi[k];
-                if (N.b < 0) {
-                    bvh4_ok = bvh4_ok && N.a < (1 << 24) && -N.b < 128;
-                    M.child[c] = ~(int32_t)leaf4.size();
-                    leaf4.push_back(N.a | (-N.b << 24));
-                } else {
-                    M.child[c] = (int32_t)q.size();
-                    q.push_back({slots[c], dep + 1});
-                }
-            }
-            n4.push_back(M);
-        }
-        // depth of every 4-wide tree (the stack bound below)
-        std::vector<int> d4(n4.size(), 0);
-        for (size_t i = 0; i < q.size(); ++i) d4[i] = q[i].second;
-        std::vector<int> owner(n4.size(), -1);  // root node4 of each node4
-        for (size_t i = 0; i < n4.size(); ++i) {
-            if (owner[i] < 0) owner[i] = (int)i;
-            for (int c = 0; c < 4; ++c)
-                if (n4[i].child[c] >= 0) owner[n4[i].child[c]] = owner[i];
-        }
-        for (size_t i = 0; i < n4.size(); ++i) {
-            const int dd = d4[i] - d4[owner[i]] + 1;
-            if (owner[i] == world_root4)
-                depth4_world = std::max(depth4_world, dd);
-            else
-                depth4_group = std::max(depth4_group, dd);
-        }
-        // 16-bit LDS stack entries: node4 ids >= 0, ~leaf < 0
-        bvh4_ok = bvh4_ok && n4.size() < 32768 && leaf4.size() < 32768;
-    }
-    // 16-B nodes (RTW_NODE16, rtw_device.h bvh_node16): the fp32 bounds times
-    // 2^k, k the largest with bvh_bound * 2^k <= 2^15, rounded outward to
-    // fp16 (exact products: a power-of-2 scale); bvh_bound becomes the
-    // largest |coordinate| the fp16 bounds stand for.  A tree the format
-    // cannot hold (siblings apart -- a node shared by two parents --, leaves
-    // of 128+ items, 2^24+ nodes or items) is not used (the flat list gives
-    // the same image).
-    std::vector<bvh_node16> dnodes16;
-    double node_scale = 1.0;
-    if (RTW_NODE16 && bvh_ok && !dnodes32.empty()) {
-        int k = 0;
-        if (bvh_bound > 0) std::frexp(0x1p15 / bvh_bound, &k), k -= 1;  // 2^k <= 2^15 / bound
-        k = std::max(-100, std::min(100, k));
-        const double up = std::ldexp(1.0, k);
-        node_scale = std::ldexp(1.0, -k);
-        auto half_out = [](double v, bool up_dir) -> uint16_t {  // fp16 bits of v rounded toward -inf / +inf
-            _Float16 h = (_Float16)v;
-            uint16_t b = __builtin_bit_cast(uint16_t, h);
-            const double hv = (double)h;
-            if (up_dir ? hv < v : hv > v) {
-                const bool neg = (b & 0x8000) != 0;
-                if ((b & 0x7fff) == 0) b = up_dir ? 0x0001 : 0x8001;  // +-0 -> the smallest subnormal outward
-                else if (neg == up_dir) b = (uint16_t)(b - 1);       // toward zero
-                else b = (uint16_t)(b + 1);                          // away from zero
-            }
-            return b;
-        };
-        bool ok16 = dnodes32.size() < (1u << 24) && ditems.size() < (1u << 24);
-        double bound16 = 0.0;
-        dnodes16.resize(dnodes32.size());
-        for (size_t n = 0; n < dnodes32.size() && ok16; ++n) {
-            const bvh_node32& M = dnodes32[n];
-            bvh_node16& Q = dnodes16[n];
-            for (int j = 0; j < 3; ++j) {
-                Q.lo[j] = half_out((double)M.lo[j] * up, false);
-                Q.hi[j] = half_out((double)M.hi[j] * up, true);
-                for (uint16_t b : {Q.lo[j], Q.hi[j]}) {
-                    const double x = (double)__builtin_bit_cast(_Float16, b);
-                    ok16 = ok16 && std::isfinite(x);
-                    bound16 = std::max(bound16, std::fabs(x) * node_scale);
-                }
-            }
-            if (M.b < 0) {
-                ok16 = ok16 && -M.b < 128 && M.a >= 0;
-                Q.w = (uint32_t)M.a | ((kNode16Leaf | (uint32_t)(-M.b)) << 24);
-            } else {
-                ok16 = ok16 && (M.b & 0x0fffffff) == M.a + 1;
-                Q.w = (uint32_t)M.a | ((uint32_t)(M.b >> 28) << 24);
-            }
-        }
-        if (ok16) {
-            bvh_bound = bound16;
-        } else {
-            bvh_ok = false;
-            dnodes16.clear();
-        }
-    }
-    // Fused group walks (rtw_device.h fused_group_bvh): the first group-BVH
-    // visit of the media walk whose group has no transforms, and the next
-    // group-BVH visit after it, are walked in one loop; each visited once.
-    int fuse_entry = -1;
-    if (RTW_FUSE_GROUPS && bvh_ok && !media.empty()) {
-        std::map<int, int> count;
-        for (int32_t v : media) ++count[v & kVisitEntry];
-        auto gbvh = [&](int e) {
-            return d->entries[e].kind == RTW_ENTRY_GROUP && dentries[e].bvh_root >= 0 && count[e] == 1;
-        };
-        int i0 = -1;
-        for (size_t i = 0; i < media.size() && i0 < 0; ++i) {
-            const int e = media[i] & kVisitEntry;
-            if (gbvh(e) && d->entries[e].n_ops == 0) i0 = (int)i;
-        }
-        for (size_t i = i0 + 1; i0 >= 0 && i < media.size(); ++i) {
-            const int e = media[i] & kVisitEntry;
-            if (gbvh(e)) {
-                fuse_entry = e;
-                media[i0] |= kVisitFuse;
-                media[i] |= kVisitMerge;
-                break;
-            }
-        }
-    }
     // device entries (dev_entry) and their op pool
     std::vector<dev_entry> dev_entries(std::max<size_t>(dentries.size(), 1));
     std::vector<dev_op> dev_ops;
@@ -2756,7 +2116,6 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         D.first_op = (int32_t)dev_ops.size();
         D.phase_material = E.phase_material, D.bvh_root = E.bvh_root, D.n_outer_ops = E.n_outer_ops;
         D.movers = entry_movers[e];
-        D.bvh_root4 = (bvh4_ok && E.bvh_root >= 0) ? root4_of[E.bvh_root] : -1;
         // the reference's -(1 / density), once per upload (a correctly
         // rounded division and a negation, as on the device)
         D.neg_inv_density = E.kind == RTW_ENTRY_MEDIUM ? -(1.0 / E.density) : 0.0;
@@ -2783,13 +2142,10 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {frames.data(), sizeof(double) * frames.size(), 0},
         {mat_aux.data(), sizeof(double) * mat_aux.size(), 0},
         {dev_ops.data(), sizeof(dev_op) * dev_ops.size(), 0},
-        {RTW_NODE16 ? (const void*)dnodes16.data() : (const void*)dnodes32.data(),
-         RTW_NODE16 ? sizeof(bvh_node16) * dnodes16.size() : sizeof(bvh_node32) * dnodes32.size(), 0},
+        {dnodes32.data(), sizeof(bvh_node32) * dnodes32.size(), 0},
         {ditems.data(), sizeof(int32_t) * ditems.size(), 0},
         {runs.data(), sizeof(world_run) * runs.size(), 0},
         {ysph.data(), sizeof(float) * ysph.size(), 0},
-        {n4.data(), sizeof(bvh_node4) * n4.size(), 0},
-        {leaf4.data(), sizeof(int32_t) * leaf4.size(), 0},
     };
     size_t total = 0;
     for (auto& p : parts) {
@@ -2818,17 +2174,9 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.ops = (const dev_op*)at(10);
     S.nodes = (const node_store*)at(11);
     S.bvh_bound = bvh_bound;
-    S.node_scale = node_scale;
-    S.fuse_entry = fuse_entry;
     S.items = (const int32_t*)at(12);
     S.runs = (const world_run*)at(13);
     S.ysph = (const float*)at(14);
-    S.nodes4 = bvh4_ok ? (const bvh_node4*)at(15) : nullptr;
-    S.leaf4 = bvh4_ok ? (const int32_t*)at(16) : nullptr;
-    S.n_nodes4 = bvh4_ok ? (int32_t)n4.size() : 0;
-    S.world_root4 = bvh4_ok ? world_root4 : -1;
-    S.lnodes4 = nullptr;
-    S.n_lnodes4 = 0;
     S.ysb_cx = ysb[0], S.ysb_cy = ysb[1], S.ysb_dy = ysb[2], S.ysb_cz = ysb[3], S.ysb_r2 = ysb[4];
     S.n_runs = (int32_t)runs.size();
     S.mv_common = mv_common ? 1 : 0;
@@ -2901,15 +2249,6 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         if (d->entries[e].bvh_root >= 0) group_depth = std::max(group_depth, depth(d->entries[e].bvh_root));
     const int world_depth = d->world_bvh_root >= 0 ? depth(d->world_bvh_root) : 0;
     h->stack_need = world_depth + group_depth + 2;
-    // 4-wide walks (walk4) stack up to three slots per level; a group walk
-    // nested in a world-BVH leaf (F_WBVH | F_GBVH) sits on the binary world
-    // walk's entries
-    {
-        const bool nested = d->world_bvh_root >= 0 && (h->features & F_GBVH);
-        const int world4 = d->world_bvh_root < 0 ? 0 : nested ? world_depth + 1 : 3 * depth4_world + 1;
-        const int group4 = (h->features & F_GBVH) ? 3 * depth4_group + 1 : 0;
-        h->stack4_need = bvh4_ok ? world4 + group4 + 1 : INT32_MAX;
-    }
     bool movers = false;
     for (int k = 0; k < d->n_prims; ++k) movers |= d->prims[k].type == RTW_PRIM_MOVING_SPHERE;
     h->desc_pin = camera_is_pinhole(d->camera);
@@ -3015,7 +2354,6 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         F.perm = p2[8].bytes ? (const int32_t*)(b2 + p2[8].off) : nullptr;
         h->f32_bytes = (uint32_t)(p2[8].off + p2[8].bytes);
         F.nodes = S.nodes;
-        F.node_scale = (float)S.node_scale;
         F.items = S.items;
         F.runs = S.runs;
         F.media = S.media;
@@ -3151,8 +2489,7 @@ bool sort_forced(bool& value) {
 // A/B).  The node count of the last launch or probe is kept for
 // rtw_scene_query.
 thread_local uint32_t g_node_packet = 0;
-// the packet holds 4-wide nodes when the walks are 4-wide (RTW_BVH4)
-constexpr size_t kPacketNodeBytes = RTW_BVH4 ? sizeof(bvh_node4) : sizeof(node_store);
+constexpr size_t kPacketNodeBytes = sizeof(node_store);
 template <int FF, int MM, bool LL>
 uint32_t node_packet(size_t shm, int n_nodes) {
     const char* e = std::getenv("RTW_LDS_NODES");
@@ -3173,6 +2510,17 @@ uint32_t node_packet(size_t shm, int n_nodes) {
     return best;
 }
 
+// The strict build's factor log holds J.flog_threads threads' paths, indexed
+// by global thread id (a path never leaves its thread in k_persist): its grid
+// is capped to fit whatever the occupancy query says (a persistent kernel
+// drains the sample queue with any grid).
+inline int strict_grid(int grid, const job_t& J) {
+#if RTW_STRICT_RADIANCE
+    return std::max(1, std::min(grid, (int)(J.flog_threads / (uint32_t)kPBlock)));
+#else
+    return grid;
+#endif
+}
 template <int FF, int MM, bool LL>
 void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t st, const scene& S, const job_t& J,
                ctrs_t* C, const char* base, uint32_t bytes, int stack_need) {
@@ -3188,9 +2536,9 @@ void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t s
             hipLaunchKernelGGL((k_persist_sort<FF, MM, LL>), dim3(persist_sort_grid<FF, MM, LL>(shm, cus)),
                                dim3(kSortBlock), shm, st, persist_args{S, J, C, base, bytes});
     } else if ((FF & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack &&
-               (RTW_BVH4 ? S.n_nodes4 > 0 : S.n_nodes < 65536)) {  // 16-bit LDS stacks
+               S.n_nodes < 65536) {  // 16-bit LDS stacks
         if (name) *name = kname("k_persist", FF, MM, LL, true);
-        uint32_t packet = node_packet<FF, MM, LL>(shm, RTW_BVH4 ? S.n_nodes4 : S.n_nodes);
+        uint32_t packet = node_packet<FF, MM, LL>(shm, S.n_nodes);
         const uint32_t off = (uint32_t)((shm + 15) & ~size_t(15));
         // a launch whose LDS does not fit would fault: no packet then
         if (packet && blocks_per_cu(reinterpret_cast<const void*>(&k_persist<FF, MM, LL, true>), kPBlock,
@@ -3199,12 +2547,12 @@ void launch_pk(bool probe, std::string* name, int cus, size_t shm, hipStream_t s
         g_node_packet = packet;
         const size_t shm2 = packet ? off + packet * kPacketNodeBytes : shm;
         if (!probe)
-            hipLaunchKernelGGL((k_persist<FF, MM, LL, true>), dim3(persist_grid<FF, MM, LL, true>(shm, cus)),
+            hipLaunchKernelGGL((k_persist<FF, MM, LL, true>), dim3(strict_grid(persist_grid<FF, MM, LL, true>(shm, cus), J)),
                                dim3(kPBlock), shm2, st, persist_args{S, J, C, base, bytes, packet, off});
     } else {
         if (name) *name = kname("k_persist", FF, MM, LL, false);
         if (!probe)
-            hipLaunchKernelGGL((k_persist<FF, MM, LL, false>), dim3(persist_grid<FF, MM, LL, false>(shm, cus)),
+            hipLaunchKernelGGL((k_persist<FF, MM, LL, false>), dim3(strict_grid(persist_grid<FF, MM, LL, false>(shm, cus), J)),
                                dim3(kPBlock), shm, st, persist_args{S, J, C, base, bytes});
     }
 }
@@ -3344,9 +2692,8 @@ bool fast_sort_enabled() {
     }();
     return on;
 }
-// the stack a persistent fp64 launch with LDS stacks needs: the 4-wide
-// walks' (RTW_BVH4) or the binary ones'
-int lst_stack_need(const handle_t* h) { return RTW_BVH4 ? h->stack4_need : h->stack_need; }
+// the stack a persistent fp64 launch with LDS stacks needs
+int lst_stack_need(const handle_t* h) { return h->stack_need; }
 void launch_fast(bool probe, const handle_t* h, hipStream_t st, const fast_args& A, std::string* name = nullptr) {
     const int f = h->features & (F_MEDIA | F_WBVH | F_GBVH);
 #ifdef RTW_SUBSET_FAST  // experiment builds (scripts/ru_kernel.sh): the list scenes' fp32 kernel only
@@ -3695,6 +3042,30 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         return RTW_OK;
     }
 
+    // execution form: persistent (paths in registers, one launch per pass)
+    // unless RTW_MODE=wavefront or no persistent instantiation covers the
+    // scene (a probe: nothing is launched); the strict build refuses the
+    // other forms here, before any allocation or launch
+    const char* mode_env = std::getenv("RTW_MODE");
+    // fp32 fast mode: its own persistent kernel (rtw_fast.h), same passes,
+    // radiance records and ordered per-pixel reduction
+    const bool fast = R.precision == RTW_PRECISION_FP32;
+    const bool pin = camera_is_pinhole(*camera);
+    bool persistent;
+    {
+        job_t J0{};
+        persistent = fast || (!(mode_env && std::string(mode_env) == "wavefront") &&
+                              launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J0, nullptr,
+                                             h->scene_base, h->shade_bytes, lst_stack_need(h), h->ysph, !h->movers,
+                                             h->S.n_lights > 0,
+                                             h->S.background != RTW_BG_GRADIENT &&
+                                                 h->S.render_type != RTW_RENDER_NORMAL,
+                                             pin));
+    }
+    if (RTW_STRICT_RADIANCE && !persistent)
+        return rtw_fail(RTW_ERR_UNSUPPORTED, "the strict-radiance build renders with the persistent kernel only "
+                                             "(RTW_MODE=wavefront or a scene without a persistent instantiation)");
+
     // pool and pass sizing
     uint32_t pool = R.wavefront_paths > 0 ? (uint32_t)R.wavefront_paths : (1u << 21);
     const size_t budget = pass_budget_samples();
@@ -3729,6 +3100,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                        reinterpret_cast<double*>(static_cast<char*>(h->camera.p) + sizeof(rtw_camera_desc)), R.nx, R.ny);
     HIPCHK(hipGetLastError());
     J.seed_mix = host_splitmix64(R.seed);
+    J.cam_pin = pin ? 1u : 0u;
     J.npix = (uint32_t)npix;
     J.nx = R.nx, J.ny = R.ny, J.row_begin = R.row_begin, J.row_step = row_step;
     J.div_npix = rtwd::udiv_magic(J.npix);
@@ -3762,12 +3134,6 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                        launch_segment(true, h->features, h->shade_mask, 0, st, h->S, J, A, FR, C, h->scene_base,
                                       h->shade_bytes);
     const int check_every = 4;
-    // execution form: persistent (paths in registers, one launch per pass)
-    // unless RTW_MODE=wavefront or no persistent instantiation covers the scene
-    const char* mode_env = std::getenv("RTW_MODE");
-    // fp32 fast mode: its own persistent kernel (rtw_fast.h), same passes,
-    // radiance records and ordered per-pixel reduction
-    const bool fast = R.precision == RTW_PRECISION_FP32;
     fast_args FA{};
     if (fast) {
         FA.S = h->F32;
@@ -3781,18 +3147,6 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
         FA.cam.time0 = (float)c.time0, FA.cam.dtime = (float)(c.time1 - c.time0);
         FA.cam.lens_radius = (float)c.lens_radius;
     }
-    const bool pin = camera_is_pinhole(*camera);
-    const bool persistent = fast || (!(mode_env && std::string(mode_env) == "wavefront") &&
-                                     launch_persist(true, h->features, h->shade_mask, 0, st, h->S, J, C,
-                                                    h->scene_base, h->shade_bytes, lst_stack_need(h), h->ysph, !h->movers,
-                                                    h->S.n_lights > 0,
-                                                    h->S.background != RTW_BG_GRADIENT &&
-                                                        h->S.render_type != RTW_RENDER_NORMAL,
-                                                    pin));
-
-    if (RTW_STRICT_RADIANCE && !persistent)
-        return rtw_fail(RTW_ERR_UNSUPPORTED, "the strict-radiance build renders with the persistent kernel only "
-                                             "(RTW_MODE=wavefront or a scene without a persistent instantiation)");
     for (uint64_t done = 0; done < (uint64_t)spp_count; done += pass_spp) {
         const uint32_t S_pass = (uint32_t)std::min<uint64_t>(pass_spp, spp_count - done);
         J.total = (uint32_t)(S_pass * npix);
@@ -3823,17 +3177,12 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
             }
             stats.launches_intersect++;
             stats.iterations++;
-#if RTW_PIXEL_MAJOR
-            hipLaunchKernelGGL(k_reduce, dim3(reduce_grid(npix)), dim3(kBlock), 0,
-                               st, J.L, (uint32_t)npix, S_pass, run);
-#else
             if (fast)
                 hipLaunchKernelGGL(k_reduce<float>, dim3(reduce_grid(npix)), dim3(kBlock), 0, st,
                                    reinterpret_cast<const float*>(J.L), (uint32_t)npix, S_pass, run);
             else
                 hipLaunchKernelGGL(k_reduce<double>, dim3(reduce_grid(npix)), dim3(kBlock), 0, st, J.L,
                                    (uint32_t)npix, S_pass, run);
-#endif
             HIPCHK(hipGetLastError());
             stats.samples += J.total;
             continue;
@@ -3912,13 +3261,8 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                 if (tail && snap.n == 0) break;
             }
         }
-#if RTW_PIXEL_MAJOR
-        hipLaunchKernelGGL(k_reduce, dim3(reduce_grid(npix)), dim3(kBlock), 0, st,
-                           J.L, (uint32_t)npix, S_pass, run);
-#else
         hipLaunchKernelGGL(k_reduce<double>, dim3(reduce_grid(npix)), dim3(kBlock), 0, st,
                            J.L, (uint32_t)npix, S_pass, run);  // the wavefront form is fp64 only
-#endif
         HIPCHK(hipGetLastError());
         stats.samples += J.total;
     }

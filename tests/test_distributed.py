@@ -71,6 +71,9 @@ def _worker(rank, world, port, mode, q):
         render_step(counting, fin, accum, canvas_t, NX, NY, SPP, timings=ms)
         local = dict(ms, kernel=10.0 * (rank + 1))  # a stand-in kernel time per rank
         phases = bench.rank_phases(local, world)
+        # a stand-in device record per rank (no GPU here): bench.device_record's fields
+        placement = bench.rank_devices(world, rank, rank, {"device": rank, "pci_bus_id": f"0000:{0x11 + rank:02x}:00",
+                                                           "name": "stand-in", "arch": "gfx950"})
         t = torch.tensor([float(stats["samples"])], dtype=torch.float64)
         dist.all_reduce(t)
         if rank == 0:
@@ -78,7 +81,7 @@ def _worker(rank, world, port, mode, q):
             _s.argv = ["bench.py", "--gpus", "2", "--steps", "1", "--scene", "cornell_box", "--nx", str(NX),
                        "--ny", str(NY), "--spp", str(SPP)]
             a = bench.parse()
-            line = bench.result_line(a, world, SPP, 0.5, float(t.item()), 1000.0, 1.0, None, phases)
+            line = bench.result_line(a, world, SPP, 0.5, float(t.item()), 1000.0, 1.0, None, phases, placement)
             q.put((line, ms))
         dist.destroy_process_group()
         return
@@ -159,3 +162,23 @@ def test_two_rank_line_carries_per_rank_phases(built):
     assert ph["render"]["min"] > 0.0  # both ranks rendered their shard
     assert line["n_gpus"] == 2 and line["value"] == round(NX * NY * SPP / 0.5 / 1e6, 3)
     assert line["config"]["parallelism"] == "spp-shard x2 + RCCL reduce"
+    # who ran where, gathered over the process group (round-5 verdict, next #5)
+    assert line["process_group"] == {"backend": "gloo", "world_size": 2, "timeout_s": bench_timeout()}
+    assert [r["rank"] for r in line["ranks"]] == [0, 1]
+    assert [r["local_rank"] for r in line["ranks"]] == [0, 1]
+    assert [r["pci_bus_id"] for r in line["ranks"]] == ["0000:11:00", "0000:12:00"]
+    assert line["distinct_devices"] == 2
+
+
+def bench_timeout():
+    import bench
+    return bench.PG_TIMEOUT_S
+
+
+def test_one_rank_placement_without_a_group():
+    import bench
+    p = bench.rank_devices(1, 0, 0, {"device": 0, "pci_bus_id": "0000:05:00", "name": "x", "arch": "gfx950"})
+    assert p["process_group"] == {"backend": None, "world_size": 1, "timeout_s": None}
+    assert p["ranks"] == [{"rank": 0, "local_rank": 0, "device": 0, "pci_bus_id": "0000:05:00", "name": "x",
+                           "arch": "gfx950"}]
+    assert p["distinct_devices"] == 1

@@ -44,7 +44,10 @@ CASES = [
 @pytest.fixture(scope="module")
 def strict(built):
     from raytracingweekend_amd import _abi, build
+    from conftest import stale
     L = _abi.load_library(build.STRICT_LIB)
+    # the strict library's own build id against the sources' with its flags
+    stale(build.STRICT_LIB.name, L.rtw_build_id().decode(), build.build_id(["-DRTW_STRICT_RADIANCE=1"]))
     if L.rtw_device_count() < 1:
         pytest.fail("no GPU visible to the HIP runtime")
     return L
