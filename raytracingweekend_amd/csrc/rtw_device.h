@@ -696,52 +696,6 @@ RTW_D bool rect_t_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, doubl
 }
 
 
-// Linear closest hit over prims [first, first+n) of one group, in list order
-// (t range (t_min, closest]) with the reference's own comparisons; the
-// primitive data are wave-uniform scalar loads.
-// (STATIC: the scene has no moving spheres, centres are center0.  WORLD: a
-// world walk, t_min = 0.001: rect tests share the direction's reciprocals.)
-template <bool STATIC = false, bool WORLD = false>
-RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, bool movers) {
-    const double fc = STATIC ? 0.0 : motion_frac(S, r.t, movers);
-    const double a = dot(r.d, r.d);  // sphere.h:50, the same for every sphere
-    constexpr bool kRcp = WORLD;
-    rect_rcp rr;
-    if (kRcp) rr = make_rect_rcp(S, r);
-    for (int i = 0; i < n; ++i) {
-        const rtw_prim q = uprim(S.prims, first + i);
-        if (is_sphere(q.type)) {
-            // sphere_t inlined so the winner is written where it is found
-            // (no per-prim merge of the running best on the common miss path)
-            const d3 oc = r.o - (STATIC ? ld3(q.p) : sphere_center(q, r.t, fc));
-            const double b = dot(oc, r.d);
-            const double c = dot(oc, oc) - q.p[9];
-            const double disc = b * b - a * c;
-            if (disc > 0) {
-                const double sq = RTW_SQRT(disc);
-                double temp = (-b - sq) / a;
-                bool ok = temp < h.t && temp > t_min;
-                if (!ok) {
-                    temp = (-b + sq) / a;
-                    ok = temp < h.t && temp > t_min;
-                }
-                if (ok) {
-                    h.t = temp;
-                    h.prim = first + i;
-                    h.rect = false;
-                }
-            }
-        } else {
-            double t;
-            if (kRcp ? rect_t_rcp(q, r, rr, t_min, h.t, t) : rect_t(q, r, t_min, h.t, t)) {
-                h.t = t;
-                h.prim = first + i;
-                h.rect = true;
-            }
-        }
-    }
-}
-
 // Shared-divisor quotients (rtw_div.h rcp_hw / div_hw) for the sphere roots
 // of a world walk: every root is (-b -+ sqrt(disc)) / dot(d, d), so a scan
 // over many spheres computes 1 / dot(d, d) once and each root pays one
@@ -776,6 +730,75 @@ RTW_D double walk_quot(double num, double den, double y, bool ok) {
     }
     return q;
 }
+
+// Linear closest hit over prims [first, first+n) of one group, in list order
+// (t range (t_min, closest]) with the reference's own comparisons; the
+// primitive data are wave-uniform scalar loads.
+// (STATIC: the scene has no moving spheres, centres are center0.  WORLD: a
+// world walk, t_min = 0.001: rect tests share the direction's reciprocals.)
+template <bool STATIC = false, bool WORLD = false>
+RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_min, hit_state& h, bool movers) {
+    const double fc = STATIC ? 0.0 : motion_frac(S, r.t, movers);
+    const double a = dot(r.d, r.d);  // sphere.h:50, the same for every sphere
+    constexpr bool kRcp = WORLD;
+    rect_rcp rr;
+    if (kRcp) rr = make_rect_rcp(S, r);
+#if RTW_AB_WSPH
+    const bool oka = WORLD && walk_ray_ok(S, r, fc) && div_hw_ok_b(a);
+    const double ya = WORLD ? rcp_hw(a) : 0.0;
+#endif
+    for (int i = 0; i < n; ++i) {
+        const rtw_prim q = uprim(S.prims, first + i);
+        if (is_sphere(q.type)) {
+            // sphere_t inlined so the winner is written where it is found
+            // (no per-prim merge of the running best on the common miss path)
+            const d3 oc = r.o - (STATIC ? ld3(q.p) : sphere_center(q, r.t, fc));
+            const double b = dot(oc, r.d);
+            const double c = dot(oc, oc) - q.p[9];
+            const double disc = b * b - a * c;
+#if RTW_AB_WSPH
+            if constexpr (WORLD) {
+                // both roots through the walk's shared 1 / a (walk_quot's
+                // rules, t_min = 0.001) and without the early returns: the
+                // winner taken by selects
+                const bool pos = disc > 0;
+                const double sq = RTW_SQRT(pos ? disc : 1.0);
+                const double t0 = walk_quot(-b - sq, a, ya, oka);
+                const double t1 = walk_quot(-b + sq, a, ya, oka);
+                const bool ok0 = t0 < h.t && t0 > t_min;
+                const bool ok1 = t1 < h.t && t1 > t_min;
+                const bool upd = pos && (ok0 || ok1);
+                h.t = upd ? (ok0 ? t0 : t1) : h.t;
+                h.prim = upd ? first + i : h.prim;
+                h.rect = upd ? false : h.rect;
+                continue;
+            }
+#endif
+            if (disc > 0) {
+                const double sq = RTW_SQRT(disc);
+                double temp = (-b - sq) / a;
+                bool ok = temp < h.t && temp > t_min;
+                if (!ok) {
+                    temp = (-b + sq) / a;
+                    ok = temp < h.t && temp > t_min;
+                }
+                if (ok) {
+                    h.t = temp;
+                    h.prim = first + i;
+                    h.rect = false;
+                }
+            }
+        } else {
+            double t;
+            if (kRcp ? rect_t_rcp(q, r, rr, t_min, h.t, t) : rect_t(q, r, t_min, h.t, t)) {
+                h.t = t;
+                h.prim = first + i;
+                h.rect = true;
+            }
+        }
+    }
+}
+
 
 // group_scan for a run of spheres that all move along y only (or not at
 // all): centre (c0.x, c0.y + p[5] * fc, c0.z).  The upload forms such runs
