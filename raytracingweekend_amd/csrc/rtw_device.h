@@ -743,10 +743,6 @@ RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_m
     constexpr bool kRcp = WORLD;
     rect_rcp rr;
     if (kRcp) rr = make_rect_rcp(S, r);
-#if RTW_AB_WSPH
-    const bool oka = WORLD && walk_ray_ok(S, r, fc) && div_hw_ok_b(a);
-    const double ya = WORLD ? rcp_hw(a) : 0.0;
-#endif
     for (int i = 0; i < n; ++i) {
         const rtw_prim q = uprim(S.prims, first + i);
         if (is_sphere(q.type)) {
@@ -756,24 +752,6 @@ RTW_D void group_scan(const scene& S, int first, int n, const ray& r, double t_m
             const double b = dot(oc, r.d);
             const double c = dot(oc, oc) - q.p[9];
             const double disc = b * b - a * c;
-#if RTW_AB_WSPH
-            if constexpr (WORLD) {
-                // both roots through the walk's shared 1 / a (walk_quot's
-                // rules, t_min = 0.001) and without the early returns: the
-                // winner taken by selects
-                const bool pos = disc > 0;
-                const double sq = RTW_SQRT(pos ? disc : 1.0);
-                const double t0 = walk_quot(-b - sq, a, ya, oka);
-                const double t1 = walk_quot(-b + sq, a, ya, oka);
-                const bool ok0 = t0 < h.t && t0 > t_min;
-                const bool ok1 = t1 < h.t && t1 > t_min;
-                const bool upd = pos && (ok0 || ok1);
-                h.t = upd ? (ok0 ? t0 : t1) : h.t;
-                h.prim = upd ? first + i : h.prim;
-                h.rect = upd ? false : h.rect;
-                continue;
-            }
-#endif
             if (disc > 0) {
                 const double sq = RTW_SQRT(disc);
                 double temp = (-b - sq) / a;
@@ -1616,30 +1594,6 @@ RTW_D double light_pdf_value(const scene& S, const rtw_light& L, d3 o, d3 v) {
     }
     if (L.kind == RTW_LIGHT_SPHERE) {  // sphere.h:88-99
         const rtw_prim& q = S.prims[L.prim];
-#if RTW_AB_LSPH
-        {
-            // sphere::hit (sphere.h:46-81) without its early returns: both
-            // roots and the pdf formed for every lane, a miss selects 0
-            const d3 oc = o - (STATIC ? ld3(q.p) : sphere_center(q, kFltMax, motion_frac(S, kFltMax, q.type >= DP_MOVING_COMMON)));
-            const double a = dot(v, v);
-            const double b = dot(oc, v);
-            const double c = dot(oc, oc) - q.p[9];
-            const double disc = b * b - a * c;
-            const bool pos = disc > 0;
-            const double sq = RTW_SQRT(pos ? disc : 1.0);
-            const double r0 = (-b - sq) / a, r1 = (-b + sq) / a;
-            const bool hit = pos && ((r0 < __builtin_inf() && r0 > 0.001) || (r1 < __builtin_inf() && r1 > 0.001));
-#if RTW_RADIANCE_FAST
-            const double cos_theta_max = RTW_SQRT(1 - q.p[9] / len2(ld3(q.p) - o));
-            const double pdf = rad_div(1.0, hit ? kTwoPi * (1.0 - cos_theta_max) : 1.0);
-#else
-            const double cos_theta_max = RTW_SQRT(1 - q.p[9] / len2(ld3(q.p) - o));  // p[9] = radius * radius
-            const double solid_angle = kTwoPi * (1.0 - cos_theta_max);
-            const double pdf = 1.0 / solid_angle;
-#endif
-            return hit ? pdf : 0.0;
-        }
-#endif
         const ray r{o, v, kFltMax};
         double t;
         // (STATIC: no moving spheres, the fraction is never read)

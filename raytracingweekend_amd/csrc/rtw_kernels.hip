@@ -968,82 +968,6 @@ void k_persist(persist_args) {
     }
 }
 
-// Split form for BVH scenes (RTW_SPLIT=2, wavefront mode): the world walk of
-// every live pool slot in a kernel of its own, as k_intersect, but with
-// k_persist's on-chip traversal state -- the BVH node packet staged in LDS
-// per 1 024-thread workgroup, 16-bit LDS stacks -- and no shading state, so
-// its registers are the walk's alone (the ray is read from the pool's SoA,
-// the hit written back as t / prim, 12 B).  k_shade then shades the slots.
-#ifndef RTW_WALK_WAVES
-#define RTW_WALK_WAVES 4
-#endif
-struct walk_args {
-    scene S;
-    paths_t P;
-    fresh_t FR;
-    double* ht;
-    int32_t* hid;
-    ctrs_t* C;
-    uint32_t lds_nodes;
-};
-// (re-read from the kernarg segment per iteration, as args_now: hoisted, the
-// scene fields the walk touches spill SGPRs into VGPR lanes)
-__device__ __forceinline__ const walk_args& walk_args_now() {
-    cptr<walk_args> p = (cptr<walk_args>)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return *(const walk_args*)p;
-}
-template <int F>
-__global__ __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RTW_WALK_WAVES)))
-void k_walk(walk_args) {
-    extern __shared__ __attribute__((aligned(16))) char s_nodes[];
-    __shared__ uint16_t s_stack[kLdsStack][kPBlock];
-    __shared__ uint32_t s_cnt[kPWaves];
-    {
-        const walk_args& W = walk_args_now();
-        const uint4* src = reinterpret_cast<const uint4*>(W.S.nodes);
-        uint4* dst = reinterpret_cast<uint4*>(s_nodes);
-        constexpr uint32_t kNode16 = (uint32_t)(sizeof(node_store) / 16);
-        for (uint32_t k = threadIdx.x; k < W.lds_nodes * kNode16; k += kPBlock) dst[k] = src[k];
-        __syncthreads();
-    }
-    const uint32_t n = walk_args_now().C->n;
-    uint32_t live = 0;
-    for (uint32_t i = blockIdx.x * kPBlock + threadIdx.x; i < n; i += gridDim.x * kPBlock) {
-        const walk_args& W = walk_args_now();
-        const uint32_t dw = W.P.depth[i];
-        if (dw == 0) continue;
-        const path_in x = load_ray(W.P, W.FR, i, dw);
-        uint32_t rng = 0u;
-        if (F & F_MEDIA) rng = x.fresh ? W.FR.rng[x.src] : W.P.rng[i];
-        uint32_t tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        lds_stack stk{&s_stack[0][tid]};
-        scene S = W.S;
-        S.lnodes = reinterpret_cast<const node_store*>(s_nodes);
-        S.n_lnodes = (int32_t)W.lds_nodes;
-        const hit_state h = world_closest<F>(S, x.r, rng, stk);
-        const walk_args& W2 = walk_args_now();
-        if (F & F_MEDIA) {
-            if (x.fresh)
-                W2.FR.rng[x.src] = rng;
-            else
-                W2.P.rng[i] = rng;
-        }
-        W2.ht[i] = h.t;
-        W2.hid[i] = h.prim;
-        ++live;
-    }
-    for (int off = 32; off > 0; off >>= 1) live += __shfl_down(live, off, 64);
-    if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = live;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int k = 0; k < kPWaves; ++k) t += s_cnt[k];
-        if (t) atomicAdd(&walk_args_now().C->segments[blockIdx.x % 8].v, t);
-    }
-}
-
 // Persistent form with material regrouping.  A wave pays for every shading
 // branch one of its lanes takes; on Cornell about half the lanes shade
 // lambertian, 30 % dielectric, 20 % emit or miss, and every wave carries all
@@ -2845,45 +2769,11 @@ void launch_shade(int mask, int grid, hipStream_t st, const scene& S, const job_
     }
 }
 
-// k_walk<F>: its grid (resident workgroups x CUs) and node packet (the
-// most nodes that keep that occupancy)
-template <int F>
-void launch_walk_t(int cus, hipStream_t st, const scene& S, const paths_t& A, const fresh_t& FR, double* ht,
-                   int32_t* hid, ctrs_t* C) {
-    const void* fn = reinterpret_cast<const void*>(&k_walk<F>);
-    const int base = blocks_per_cu(fn, kPBlock, 0);
-    uint32_t packet = 0;
-    for (uint32_t k = 32; k <= (uint32_t)S.n_nodes + 31; k += 32) {
-        const uint32_t kk = std::min<uint32_t>(k, (uint32_t)S.n_nodes);
-        if (blocks_per_cu(fn, kPBlock, kk * kPacketNodeBytes) < base) break;
-        packet = kk;
-        if (kk == (uint32_t)S.n_nodes) break;
-    }
-    g_node_packet = packet;
-    hipLaunchKernelGGL(k_walk<F>, dim3(std::max(1, base) * cus), dim3(kPBlock), packet * kPacketNodeBytes, st,
-                       walk_args{S, A, FR, ht, hid, C, packet});
-}
-bool walk_split() {
-    const char* e = std::getenv("RTW_SPLIT");
-    return e && std::atoi(e) == 2;
-}
-
 // one traversal kernel per scene-feature combination (a world BVH never
 // coexists with media: validate_desc)
 void launch_intersect(int f, int grid, hipStream_t st, const scene& S, const paths_t& A, const fresh_t& FR,
                       double* ht, int32_t* hid,
-                      ctrs_t* C, int cus = 0, int stack_need = 1 << 30) {
-    if (cus > 0 && walk_split() && (f & (F_WBVH | F_GBVH)) && stack_need <= kLdsStack && S.n_nodes < 65536) {
-        switch (f) {
-#ifndef RTW_SUBSET
-        case F_WBVH: launch_walk_t<F_WBVH>(cus, st, S, A, FR, ht, hid, C); return;
-        case F_GBVH: launch_walk_t<F_GBVH>(cus, st, S, A, FR, ht, hid, C); return;
-        case F_WBVH | F_GBVH: launch_walk_t<F_WBVH | F_GBVH>(cus, st, S, A, FR, ht, hid, C); return;
-#endif
-        case F_MEDIA | F_GBVH: launch_walk_t<F_MEDIA | F_GBVH>(cus, st, S, A, FR, ht, hid, C); return;
-        default: break;
-        }
-    }
+                      ctrs_t* C) {
     switch (f) {
 #define RTW_CASE(F)                                                                               \
     case F:                                                                                       \
@@ -3328,8 +3218,7 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
                     if (!event_at(h, e1)) return rtw_fail(RTW_ERR_HIP, "hipEventCreate failed");
                     HIPCHK(hipEventRecord(h->events[e0], st));
                 }
-                launch_intersect(h->features & (F_MEDIA | F_WBVH | F_GBVH), grid, st, h->S, A, FR, ht, hid, C, h->cus,
-                                 lst_stack_need(h));
+                launch_intersect(h->features, grid, st, h->S, A, FR, ht, hid, C);
                 if (timed) {
                     HIPCHK(hipEventRecord(h->events[e1], st));
                     isect_ev.push_back({e0, e1});
