@@ -124,7 +124,7 @@ RTW_HD d3 operator-(d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 RTW_HD d3 operator*(d3 a, d3 b) { return d3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 RTW_HD d3 operator*(d3 a, double s) { return d3{a.x * s, a.y * s, a.z * s}; }
 // d3 / double (vec3.h operator/): three IEEE divisions.  (Sharing one
-// reciprocal behind a range vote measured T -3.3 %: DESIGN.md §4.2b.)
+// reciprocal behind a range vote measured T -3.3 %: EXPERIMENTS.md.)
 RTW_HD d3 operator/(d3 a, double s) { return d3{a.x / s, a.y / s, a.z / s}; }
 RTW_HD d3 operator-(d3 a) { return d3{-a.x, -a.y, -a.z}; }
 // a / b for a quantity that only scales radiance (RTW_RADIANCE_RCP)
@@ -139,7 +139,7 @@ RTW_HD double len2(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
 // fp64 square roots as rtw_div.h's sqrt_w (the compiler's own sequence
 // without its range scaling and class fixup, taken when the whole wave is in
 // range; bit for bit the same value) or sqrt_core where the range is known
-// (1 - a canonical draw).  Measured T +0.5 %, C5 +1.7 %.
+// (1 - a canonical draw).  Measured T +0.5 %, C5 +1.7 % (EXPERIMENTS.md).
 #if defined(__HIP_DEVICE_COMPILE__)
 #define RTW_SQRT(x) sqrt_w(x)
 #define RTW_SQRT_POS(x) sqrt_core(x)  // x in [2^-766, 2^1024): callers argue it
@@ -317,7 +317,7 @@ struct bvh_node32;
 // Device BVH node format (rtw_scene_upload writes it, node_at reads it):
 // 32-B nodes with fp32 bounds.  (16-B fp16 nodes, twice the nodes per LDS
 // packet, measured C5 -6 %, C3 -9 %: the packet already holds every node of
-// C3 and C5 and the fp16 decode costs more)
+// C3 and C5 and the fp16 decode costs more; EXPERIMENTS.md.)
 using node_store = bvh_node32;
 struct world_run {
     int32_t entry, first_prim, n_prims, movers;  // movers: the prims hold DP_MOVING_COMMON*
@@ -341,7 +341,7 @@ struct dev_op {
 };
 // The media walk (scene::media) lists entry indices in visit order.
 // (A boundary cache for a medium's second visit measured C5 -8 %, and fused
-// walks of two group trees -11 %: DESIGN.md §4.2b.)
+// walks of two group trees -11 %: EXPERIMENTS.md.)
 constexpr int32_t kVisitEntry = (1 << 20) - 1;
 struct scene {
     const rtw_prim* prims;
@@ -1007,7 +1007,7 @@ RTW_D void arbitrate_a(const scene& S, int pi, const ray& r, double t_min, hit_s
 }
 
 // The items of a group-BVH leaf.  (Reciprocals shared across the leaf's
-// boxes and spheres measured C5 -7 %: 10 more spilled VGPRs, §4.2b.)
+// boxes and spheres measured C5 -7 %: 10 more spilled VGPRs, EXPERIMENTS.md.)
 RTW_D void leaf_items(const scene& S, int la, int lc, const ray& r, double t_min, hit_state& h, double fc) {
     for (int k = 0; k < lc; ++k) arbitrate_item(S, S.items[la + k], r, t_min, h, fc);
 }
@@ -1198,7 +1198,7 @@ RTW_D bool expand_children(const scene& S, const slab_ray& sr, float t0, float t
 
 // BVH over the prims of one group (items = prim indices).  (Packet walks of
 // a wave-uniform root, 4-wide nodes and fused walks of two group trees all
-// measured slower: DESIGN.md §4.2, §4.2b.)
+// measured slower: EXPERIMENTS.md.)
 template <class STK>
 RTW_D void group_bvh(const scene& S, int root, const ray& r, double t_min, hit_state& h, STK& stk, int base,
                      bool movers) {

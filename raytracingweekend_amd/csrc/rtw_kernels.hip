@@ -775,7 +775,7 @@ __device__ __forceinline__ const persist_args& args_now() {
 // The loop-carried ray stays in registers: every form that parked it in LDS
 // (the whole ray with lane-direct camera samples, or its origin beside
 // smaller batches) took that LDS from the node packet or the batches and
-// measured slower than the spills it removed.
+// measured slower than the spills it removed (EXPERIMENTS.md).
 template <int F, int M, bool LDS, bool LST = false>
 __global__ __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(RTW_PERSIST_WAVES(F, M))))
 void k_persist(persist_args) {
@@ -982,7 +982,7 @@ void k_persist(persist_args) {
 // that take camera samples next: they sit together at the block's top,
 // beside the idle ones, so ray generation runs lane-full in one or two waves.
 // (Cheap keys between the expensive ones measured T -7 %, and sorting
-// lambertian hits on their mixture choice T -1 %: DESIGN.md §4.2c.)
+// lambertian hits on their mixture choice T -1 %: EXPERIMENTS.md.)
 enum { K_LAMB = 0, K_DIEL, K_METAL, K_ISO, K_EMIT, K_MISS, K_IDLE, K_N };
 
 // Ray generation threshold: a wave takes camera samples only when at least
@@ -998,7 +998,7 @@ enum { K_LAMB = 0, K_DIEL, K_METAL, K_ISO, K_EMIT, K_MISS, K_IDLE, K_N };
 #define RTW_REFILL_MIN 8
 #endif
 // Paths regrouped together (one workgroup).  (128 or 512 measured T -15 % /
-// -13 %)
+// -13 %, EXPERIMENTS.md.)
 constexpr int kSortBlock = 256;
 constexpr int kSortWaves = kSortBlock / 64;
 // The counting sort's block prefix from a key-major
@@ -1277,7 +1277,7 @@ constexpr int FF_NONOISE = 1 << 12;
 #endif
 // The path -- ray, throughput, engine, depth, sample id -- is in registers.
 // (Throughput and sample id in LDS home slots halve the media kernel's spill
-// stores but take a third of its node packet: -1 %)
+// stores but take a third of its node packet: -1 %, EXPERIMENTS.md.)
 template <int F, bool LST>
 __global__ __launch_bounds__(rtwf::fast_block(F)) __attribute__((amdgpu_waves_per_eu(RTW_FAST_BVH_WAVES)))
 void k_fast(fast_args) {

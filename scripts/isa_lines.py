@@ -6,7 +6,7 @@
 inline chain (e.g. --outer rtw_kernels.hip: which call site of the kernel
 body the instruction belongs to -- camera sample, world walk, sort prefix,
 shading) instead of the innermost line.  That view found the counting
-sort's block prefix (~67 VALU per wave-iteration).
+sort's block prefix (~67 VALU per wave-iteration, EXPERIMENTS.md).
 
 Each v_* instruction is weighted by its measured issue cost on gfx950
 (scripts/valu_rates.hip, profiles/r01/valu_rates.log: fp64 ~4.7 cycles per wave

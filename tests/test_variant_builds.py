@@ -2,7 +2,7 @@
 hipcc's gfx950 front end, -fsyntax-only over the one-kernel subset builds of
 scripts/ru_kernel.sh, templates instantiated): the strict-radiance build,
 the section profiler, and the occupancy knobs.  The A/B forms measured and
-rejected (DESIGN.md §4.2-§4.2c) were removed from the sources in round 6;
+rejected (EXPERIMENTS.md) were removed from the sources in round 6;
 git history and the committed A/B logs keep them.  The default build is
 compiled in full by build() and run by the GPU suite; the strict build
 likewise (tests/test_gpu_strict.py)."""
