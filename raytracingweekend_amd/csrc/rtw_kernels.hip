@@ -574,7 +574,7 @@ __device__ __forceinline__ bool shade_one(const scene& S, const job_t& J, const 
         return true;
     }
     if (out == SEG_END_ZERO) {
-        L = d3{0, 0, 0};
+        L = thr * 0.0;  // (NaN / inf throughputs give NaN, as the reference's products do)
         return true;
     }
     const d3 nt = thr * w;
@@ -944,8 +944,10 @@ void k_persist(persist_args) {
                 },
                 [&](const d3& E) { radiance(d3{s_thr[0][me], s_thr[1][me], s_thr[2][me]} * E); },
                 [&]() {
+                    // thr * 0, not 0: the reference multiplies its factors into
+                    // the 0 color() returns, so a non-finite throughput gives NaN
                     const double z = in_place<0>();
-                    radiance(d3{z, z, z});
+                    radiance(d3{s_thr[0][me], s_thr[1][me], s_thr[2][me]} * z);
                 });
 #endif
             const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0,
@@ -1207,8 +1209,10 @@ void k_persist_sort(persist_args) {
                     radiance(d3{s_thr[0][home], s_thr[1][home], s_thr[2][home]} * E);
                 },
                 [&]() {
+                    // thr * 0 (k_persist's reason: NaN / inf throughputs give NaN)
+                    const uint32_t home = x_home[me];
                     const double z = in_place<0>();
-                    radiance(d3{z, z, z});
+                    radiance(d3{s_thr[0][home], s_thr[1][home], s_thr[2][home]} * z);
                 });
             const int out = shade_core<M, (F & F_STATIC) != 0, (F & F_LIGHTS) != 0, (F & F_BLACK) != 0,
                                        (F & F_NOLIGHTS) != 0>(SS, x, x_t[me], x_prim[me], sk, pf);

@@ -264,3 +264,33 @@ def test_bvh_equals_flat_at_size(gpu, scene, nx, ny, spp):
     (flat, st_flat), (tree, st_tree) = out
     assert st_flat["segments"] == st_tree["segments"]
     assert np.array_equal(flat, tree), f"max diff {np.abs(flat - tree).max()}"
+
+
+@pytest.mark.parametrize("bvh", [False, True])
+def test_degenerate_camera_matches_oracle(gpu, bvh):
+    """A camera whose u, v are not finite (vup parallel to the view direction:
+    u = unit_vector(cross(vup, w)) = 0 / 0, camera.h:36-50) with no lens: the
+    reference's offset u * rd.x + v * rd.y is NaN, so are its rays.  The
+    kernels' pinhole shortcut (which skips the offset) must not apply
+    (camera_is_pinhole requires finite u, v): NaN rays traverse
+    and shade as the reference's do -- same traversal count, same sums, NaN
+    where the oracle has NaN."""
+    from raytracingweekend_amd import _abi
+    nx, ny, spp, depth = 24, 24, 2, 50
+    scene = "cornell_box" if not bvh else "random_balls"
+    sd = gpu.SceneDesc(scene, nx / ny, use_bvh=bvh)
+    cam = _abi.rtw_camera_desc.from_buffer_copy(sd.camera)
+    for k in range(3):
+        cam.u[k] = float("nan")
+        cam.v[k] = float("nan")
+    cam.lens_radius = 0.0
+    ds = gpu.DeviceScene(sd)
+    try:
+        acc, st = ds.render_accumulate(nx, ny, spp, depth, seed=5, camera=cam)
+    finally:
+        ds.close()
+    ref, seg = oracle_sums(gpu.SceneDesc(scene, nx / ny), nx, ny, spp, depth, seed=5, camera=cam)
+    assert st["segments"] == seg, "device-counted traversals differ from the oracle's"
+    assert np.array_equal(np.isnan(acc), np.isnan(ref)), "NaN channels differ from the oracle's"
+    fin = ~np.isnan(ref)
+    assert np.all(np.abs(acc[fin] - ref[fin]) <= TOL * spp)
