@@ -1722,7 +1722,7 @@ RTW_D double schlick_r0(double cosine, double r0) { return r0 + (1 - r0) * pow5(
 // the offset not computed.  The draws, the time and the ray are the
 // reference's (camera.h:36-50).
 RTW_D ray camera_ray(const rtw_camera_desc& c, double s, double t, uint32_t& rng, bool pin) {
-    d3 p;  // (pin is wave-uniform: the job's)
+    d3 p;  // (pin is wave-uniform: the job's or the camera's)
     {
         constexpr float k2Rf = (float)(2.0 / kCanonR);
         auto lead = [&](uint32_t raw) { return __builtin_fmaf((float)(raw - 1u), k2Rf, -1.0f); };

@@ -142,6 +142,14 @@ __device__ __forceinline__ void sample_coords(const job_t& J, uint32_t q, int& i
 
 // Render-loop body RayTracingWeekend.cpp:227-231 for sample q: jitter,
 // camera::get_ray -> staging entry k.
+// JPIN: the pinhole shortcut applies per the job's host-computed flag
+// (J.cam_pin), else per the device camera's own lens_radius == 0 and nonzero
+// origin -- the host gives a lens-less camera with a non-finite u or v a NaN
+// lens_radius in the device copy, so both say the same.  (The two forms
+// measure differently through code layout alone: J.cam_pin T +0.6 %, the
+// camera test C3 +1.5 %, profiles/r06/ab_r6h_*.log; each kernel takes its
+// better one.)
+template <bool JPIN = true>
 __device__ __forceinline__ ray camera_sample(const job_t& J, uint32_t q, uint32_t& rng) {
     int i, j, s;
     sample_coords(J, q, i, j, s);
@@ -177,7 +185,9 @@ __device__ __forceinline__ ray camera_sample(const job_t& J, uint32_t q, uint32_
     c.time0 = ld(&cp->time0);
     c.time1 = ld(&cp->time1);
     c.lens_radius = ld(&cp->lens_radius);
-    return camera_ray(c, u, v, rng, J.cam_pin != 0);
+    const bool pin = JPIN ? J.cam_pin != 0
+                          : (c.lens_radius == 0.0 && c.origin[0] != 0.0 && c.origin[1] != 0.0 && c.origin[2] != 0.0);
+    return camera_ray(c, u, v, rng, pin);
 }
 
 __device__ __forceinline__ void raygen(const job_t& J, const fresh_t& F, uint32_t k, uint32_t q) {
@@ -854,7 +864,7 @@ void k_persist(persist_args) {
                     if (left) open = false;
                     if (got) {  // (lanes >= NB get no id)
                         uint32_t rng;
-                        const ray r = camera_sample(J, q, rng);
+                        const ray r = camera_sample<false>(J, q, rng);
                         if constexpr (!PIN) B.ox[ln] = r.o.x, B.oy[ln] = r.o.y, B.oz[ln] = r.o.z;
                         B.dx[ln] = r.d.x, B.dy[ln] = r.d.y, B.dz[ln] = r.d.z;
                         B.tm[ln] = r.t;
@@ -3097,6 +3107,16 @@ extern "C" int rtw_render_accumulate(void* handle, const rtw_camera_desc* camera
 
     job_t J;
     h->cam_host = *camera;
+    // camera_sample<false>'s pinhole test reads lens_radius and the origin; a
+    // lens-less camera whose u or v is not finite gets lens_radius NaN in the
+    // device copy: rd = NaN * p, so its offset is NaN as the reference's
+    // u * rd.x + v * rd.y is (the same all-NaN rays, the same draws), and the
+    // shortcut does not apply
+    {
+        bool uv = true;
+        for (int k = 0; k < 3; ++k) uv = uv && std::isfinite(camera->u[k]) && std::isfinite(camera->v[k]);
+        if (!uv && h->cam_host.lens_radius == 0.0) h->cam_host.lens_radius = __builtin_nan("");
+    }
     if ((rc = h->camera.ensure(sizeof(rtw_camera_desc) + 2 * sizeof(double)))) return rc;
     HIPCHK(hipMemcpyAsync(h->camera.p, &h->cam_host, sizeof(rtw_camera_desc), hipMemcpyHostToDevice, st));
     J.cam = static_cast<const rtw_camera_desc*>(h->camera.p);
