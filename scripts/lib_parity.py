@@ -15,13 +15,14 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 CASES = {"cornell_box": (96, 96, 64, False), "book2_final": (64, 64, 16, True),
-         "random_balls": (96, 64, 16, True), "light_sample": (64, 64, 32, False)}
+         "random_balls": (96, 64, 16, True), "light_sample": (64, 64, 32, False),
+         "random_balls_flat": (96, 64, 16, False)}
 
 
 def _one(scene, out, precision):
     from raytracingweekend_amd.render import DeviceScene, SceneDesc
     nx, ny, spp, bvh = CASES[scene]
-    ds = DeviceScene(SceneDesc(scene, nx / ny, bvh), 0)
+    ds = DeviceScene(SceneDesc(scene.replace("_flat", ""), nx / ny, bvh), 0)
     try:
         accum, _ = ds.render_accumulate(nx, ny, spp, 50, 7, precision=precision)
     finally:
