@@ -359,10 +359,10 @@ RTW_D bool slab(const bvh_node32& nd, const slab_rayf& s, float t0, float t1) {
 }
 // (explicit address spaces, as rtwd::node_at: an LDS read for packet nodes,
 // a global read for the rest)
-// PALL: the all-in-packet shortcut is compiled in; the
-// media kernel leaves it out (its packet never holds every node at two
-// workgroups per CU, and the branch cost it a spilled register: C5 fp32
-// -1.4 %, profiles/r05/ab_r5f_fpall.log)
+// PALL: the all-in-packet shortcut is compiled in (every fp32 BVH kernel
+// since round 6; with 16-entry stacks the media kernel's packet never held
+// every node and the branch cost it a spilled register: C5 fp32 -1.4 %,
+// profiles/r05/ab_r5f_fpall.log)
 template <bool PALL = true>
 RTW_D bvh_node32 node_at(const fscene& S, int i) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -400,15 +400,25 @@ constexpr int kFastBlock = 1024;
 // packet) 472; 768 at 6 (spill-free, every node in the packet, its fetch
 // shortcut) 751.  1 024 stays.
 constexpr int fast_block(int F) { return kFastBlock; }
-// the all-in-packet node fetch (node_at<PALL>): not in the media kernel (its
-// packet holds every node only at smaller workgroups)
-constexpr bool fast_pall(int F) { return (F & rtwd::F_MEDIA) == 0; }
+// LDS stack entries per lane.  The media kernel's walks are group walks
+// from an empty stack (a scene with media has no world BVH), which hold at
+// most D entries for a tree of depth D (launch_fast: group_depth), so 12
+// entries serve Book 2's trees (depths 10 and 12) where the general bound
+// (world + group depth + 2) asks for 16.  The 8 KB this frees per
+// workgroup grows the node packet from 1 534 to all 1 668 of Book 2's nodes
+// at two 1 024-thread workgroups per CU, and every node is then an LDS
+// read (node_at<PALL>): C5 fp32 32-spp slice 856 vs 828 Msamples/s
+// (+3.4 %, profiles/r06/ab_r6o_C5f.log; bit-identical, parity_r6o_mstack.log).
+constexpr int kMediaStack = 12;
+constexpr int fast_stack(int F) { return (F & rtwd::F_MEDIA) ? kMediaStack : rtwd::kLdsStack; }
+// the all-in-packet node fetch (node_at<PALL>, a wave-uniform test)
+constexpr bool fast_pall(int F) { return true; }
 
 // traversal stacks: a column of 16-bit node ids per lane in LDS (column
 // stride: the workgroup size), or a private array
-template <int BLK>
+template <int BLK, int CAP = rtwd::kLdsStack>
 struct lds_stackf_t {
-    static constexpr int cap = rtwd::kLdsStack;
+    static constexpr int cap = CAP;
     uint16_t* p;
     RTW_D uint16_t& at(int i) { return p[i * BLK]; }
 };

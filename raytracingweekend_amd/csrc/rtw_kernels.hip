@@ -1300,7 +1300,7 @@ void k_fast(fast_args) {
     constexpr int kFB = fast_block(F);
     constexpr int kFW = kFB / 64;
     extern __shared__ __attribute__((aligned(16))) char s_nodes[];
-    __shared__ uint16_t s_stack[LST ? kLdsStack : 1][kFB];
+    __shared__ uint16_t s_stack[LST ? fast_stack(F) : 1][kFB];
     __shared__ uint32_t s_cnt[kFW];
     if (LST) {  // the BVH node packet (the top levels of every tree)
         const fast_args& A = fast_args_now();
@@ -1362,7 +1362,7 @@ void k_fast(fast_args) {
         if (depth == 0) continue;
         fhit h;
         if constexpr (LST) {
-            lds_stackf_t<kFB> stk{&s_stack[0][threadIdx.x]};
+            lds_stackf_t<kFB, fast_stack(F)> stk{&s_stack[0][threadIdx.x]};
             const fast_args& A = fast_args_now();
             fscene S = A.S;
             S.lnodes = reinterpret_cast<const node_store*>(s_nodes);
@@ -1819,6 +1819,7 @@ struct handle_t {
     int grid = 2048;
     int cus = 256;
     int stack_need = 0;  // deepest BVH stack a traversal of this scene can use
+    int group_depth = 0;  // depth of its deepest group BVH
     // BVH boxes of moving spheres cover the desc camera's shutter only
     bool bvh_motion = false;
     double shutter0 = 0.0, shutter1 = 0.0;
@@ -2263,6 +2264,13 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         if (d->entries[e].bvh_root >= 0) group_depth = std::max(group_depth, depth(d->entries[e].bvh_root));
     const int world_depth = d->world_bvh_root >= 0 ? depth(d->world_bvh_root) : 0;
     h->stack_need = world_depth + group_depth + 2;
+    // A walk from an empty stack that pops one node and pushes both children
+    // of an inner one holds at most D entries for a tree of depth D (the
+    // entry at stack position j has depth >= j + 1: true for the root at 0,
+    // and an inner node of depth k popped from position k' <= k - 1 puts
+    // depth-(k + 1) children at k' and k' + 1).  The fp32 media kernel's
+    // group walks are such walks (launch_fast).
+    h->group_depth = group_depth;
     bool movers = false;
     for (int k = 0; k < d->n_prims; ++k) movers |= d->prims[k].type == RTW_PRIM_MOVING_SPHERE;
     h->desc_pin = camera_is_pinhole(d->camera);
@@ -2733,7 +2741,10 @@ void launch_fast(bool probe, const handle_t* h, hipStream_t st, const fast_args&
                 : launch_fast_sort_t<0, false>(probe, name, h->cus, st, A, base, h->f32_bytes);
         return;
     }
-    const bool lst = (f & (F_WBVH | F_GBVH)) && h->stack_need <= kLdsStack && h->S.n_nodes < 65536;
+    // (media scenes have no world BVH: their walks are group walks from an
+    // empty stack, group_depth entries deep)
+    const int need = (f & F_MEDIA) ? h->group_depth : h->stack_need;
+    const bool lst = (f & (F_WBVH | F_GBVH)) && need <= rtwf::fast_stack(f) && h->S.n_nodes < 65536;
     if (f == F_WBVH && lst && !(h->shade_mask & SF_NOISE)) {  // random_balls + BVH: no marble texture
         launch_fast_t<F_WBVH | FF_NONOISE, true>(probe, name, h->cus, st, A);
         return;

@@ -185,6 +185,50 @@ def test_bvh_build_is_well_formed(render_mod):
                     assert sum(1 for it in seen if it & _abi.RTW_ITEM_BOX) == 400
 
 
+def _depth(d, root):
+    best, todo = 0, [(root, 1)]
+    while todo:
+        n, k = todo.pop()
+        best = max(best, k)
+        if d.bvh_nodes[n].count == 0:
+            todo += [(d.bvh_nodes[n].left, k + 1), (d.bvh_nodes[n].right, k + 1)]
+    return best
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_group_walk_stack_depth_bound(render_mod, seed):
+    """The fp32 media kernel sizes its LDS stacks by the deepest group BVH
+    (rtw_fast.h kMediaStack, rtw_kernels.hip launch_fast): a walk from an
+    empty stack that pops one node and pushes both children of an inner one
+    never holds more than D entries for a tree of depth D.  Replays that walk
+    (rtw_fast.h group_bvh pushes right, then left; the fp64 walks push the
+    nearer child last, so the order here is also drawn at random) on Book 2's
+    group trees, with slab tests passing at random and always, and checks the
+    bound is never passed; Book 2's trees fit the 12-entry stacks."""
+    import random
+    rnd = random.Random(seed)
+    d = render_mod.SceneDesc("book2_final", 1.0, use_bvh=True).desc
+    roots = [d.entries[e].bvh_root for e in range(d.n_entries) if d.entries[e].bvh_root >= 0]
+    assert d.world_bvh_root < 0 and len(roots) == 2
+    for root in roots:
+        D = _depth(d, root)
+        assert D <= 12
+        for p_pass in (1.0, 0.7, 0.4):
+            for shuffled in (False, True):
+                sp_max, stack = 0, [root]
+                while stack:
+                    nd = d.bvh_nodes[stack.pop()]
+                    if p_pass < 1.0 and rnd.random() > p_pass:
+                        continue
+                    if nd.count == 0:
+                        kids = [nd.right, nd.left]
+                        if shuffled and rnd.random() < 0.5:
+                            kids.reverse()
+                        stack += kids
+                        sp_max = max(sp_max, len(stack))
+                assert sp_max <= D
+
+
 def test_unknown_scene_is_an_error(render_mod):
     from raytracingweekend_amd import RtwError
     with pytest.raises(RtwError, match="unknown scene"):
