@@ -500,7 +500,8 @@ RTW_D fhit world_closest(const fscene& S, const fray& r, uint32_t& rng, STK& stk
                 continue;
             }
             for (int k = 0; k < -nd.b; ++k) {
-                const int it = S.items[nd.a + k];
+                // (a one-item world leaf holds its item: launch-time fp32 nodes)
+                const int it = nd.b == -1 ? nd.a : S.items[nd.a + k];
                 if (it < 0) {  // a plain one-prim entry: ~prim
                     arbitrate(S, ~it, r, kTMinF, h);
                     continue;

@@ -2031,10 +2031,12 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     // World-BVH leaves reference entries; a plain one-prim entry's item is
     // replaced by ~prim so the walk tests the prim without reading the entry.
     std::vector<int32_t> ditems(d->bvh_items, d->bvh_items + d->n_bvh_items);
+    std::vector<char> world_node(d->n_bvh_nodes, 0);  // (the fp32 nodes' inline world leaves)
     if (d->world_bvh_root >= 0) {
         std::vector<int> todo{d->world_bvh_root};
         while (!todo.empty()) {
             const rtw_bvh_node& N = d->bvh_nodes[todo.back()];
+            world_node[todo.back()] = 1;
             todo.pop_back();
             if (N.count == 0) {
                 todo.push_back(N.left);
@@ -2071,6 +2073,14 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     // a BVH whose bounds are not finite within 2^90 is not used at all (the
     // flat list gives the same image)
     std::vector<bvh_node32> dnodes32(dnodes.size());
+    // The fp32 kernels' copy of the nodes: a one-item leaf of the world BVH
+    // holds its item (entry or ~prim) in a instead of its index into the
+    // item array, so the fp32 world walk (rtw_fast.h world_closest) reaches
+    // the prim with one dependent load less per leaf.  Measured (1 MI355X,
+    // A/B, profiles/r06/ab_r6r_C3f.log; bit-identical, parity_r6r_inl2.log):
+    // C3 fp32 +1.9 %.  The fp64 walks keep the shared form: the same inline
+    // leaves there measured C3 -0.7 % (ab_r6r_C3.log).
+    std::vector<bvh_node32> dnodes32f(dnodes.size());
     double bvh_bound = 0.0;
     bool bvh_ok = dnodes.size() < (1u << 28);
     for (size_t k = 0; k < dnodes.size(); ++k) {
@@ -2087,6 +2097,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         }
         M.a = N.left;
         M.b = N.count > 0 ? -N.count : (N.right | (N.pad << 28));
+        dnodes32f[k] = M;
+        if (world_node[k] && N.count == 1) dnodes32f[k].a = ditems[N.left];
     }
     // Breadth-first numbering from all roots together (the world BVH's, then
     // every group's, in entry order): nodes [0, k) are then the top levels of
@@ -2106,16 +2118,20 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             if (N.count == 0) enqueue(N.left), enqueue(N.right);
         }
         for (size_t n = 0; n < dnodes32.size(); ++n) enqueue((int)n);  // unreachable nodes keep a slot
-        std::vector<bvh_node32> bfs(dnodes32.size());
-        for (size_t n = 0; n < dnodes32.size(); ++n) {
-            bvh_node32 M = dnodes32[n];
-            if (M.b >= 0) {  // inner: renumber both children, keep the split bits
-                M.a = newid[M.a];
-                M.b = newid[M.b & 0x0fffffff] | (M.b & ~0x0fffffff);
+        auto renumber = [&](std::vector<bvh_node32>& nodes) {
+            std::vector<bvh_node32> bfs(nodes.size());
+            for (size_t n = 0; n < nodes.size(); ++n) {
+                bvh_node32 M = nodes[n];
+                if (M.b >= 0) {  // inner: renumber both children, keep the split bits
+                    M.a = newid[M.a];
+                    M.b = newid[M.b & 0x0fffffff] | (M.b & ~0x0fffffff);
+                }
+                bfs[newid[n]] = M;
             }
-            bfs[newid[n]] = M;
-        }
-        dnodes32.swap(bfs);
+            nodes.swap(bfs);
+        };
+        renumber(dnodes32);
+        renumber(dnodes32f);
         if (world_root >= 0) world_root = newid[world_root];
         for (rtw_entry& E : dentries)
             if (E.bvh_root >= 0) E.bvh_root = newid[E.bvh_root];
@@ -2352,6 +2368,8 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             {fr32.data(), sizeof(float) * fr32.size(), 0},
             {d->lights, sizeof(rtw_light) * d->n_lights, 0},
             {d->has_perlin ? d->perlin_perm : nullptr, d->has_perlin ? sizeof(int32_t) * 768 : 0, 0},
+            // (after the staged prefix)
+            {dnodes32f.data(), sizeof(bvh_node32) * dnodes32f.size(), 0},
         };
         size_t tot = 0;
         for (auto& x : p2) {
@@ -2375,7 +2393,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         F.lights = p2[7].bytes ? (const rtw_light*)(b2 + p2[7].off) : nullptr;
         F.perm = p2[8].bytes ? (const int32_t*)(b2 + p2[8].off) : nullptr;
         h->f32_bytes = (uint32_t)(p2[8].off + p2[8].bytes);
-        F.nodes = S.nodes;
+        F.nodes = S.nodes ? (const node_store*)(b2 + p2[9].off) : nullptr;
         F.items = S.items;
         F.runs = S.runs;
         F.media = S.media;
