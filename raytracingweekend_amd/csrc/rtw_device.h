@@ -373,6 +373,10 @@ struct scene {
     // and r^2 of the filtered spheres
     const float* ysph;
     float ysb_cx, ysb_cy, ysb_dy, ysb_cz, ysb_r2;
+    // box items' planes: for the first rect i of a box, {x0, x1, y0, y1, z0,
+    // z1} at boxes[8 i] (rtw_scene_upload, when every box's six rects match
+    // them; nullptr: the walks read the rects)
+    const double* boxes;
     // BVH node packets staged in LDS: the upload numbers the nodes of every
     // BVH breadth-first from all roots together, so nodes [0, n_lnodes) are
     // the top levels of every tree; the persistent BVH kernels copy them to
@@ -663,8 +667,8 @@ RTW_D rect_rcp make_rect_rcp(const scene& S, const ray& r) {
 // A/B, profiles/r05/ab_r5u_rect_branchless.log; bit-identical images): T
 // 4 811 vs 4 747 (+1.3 %); in the BVH leaves' box faces (mostly missed, the
 // early return skips their a, b) C5 -1.2 %, so those keep it.
-template <int K, int A, int B, bool BL = false>
-RTW_D bool rect_axis_rcp(const rtw_prim& q, const ray& r, const rect_rcp& rr, double t0, double t1,
+template <int K, int A, int B, bool BL = false, class Q = rtw_prim>
+RTW_D bool rect_axis_rcp(const Q& q, const ray& r, const rect_rcp& rr, double t0, double t1,
                          double& t_out) {
     const double ok = K == 0 ? r.o.x : (K == 1 ? r.o.y : r.o.z);
     const double od = K == 0 ? r.d.x : (K == 1 ? r.d.y : r.d.z);
@@ -959,8 +963,38 @@ RTW_D rect_rcp make_rect_rcp_t(const scene& S, const ray& r, double t_min) {
     for (int k = 0; k < 3; ++k) rr.ok[k] = rr.ok[k] && tmin_ok;
     return rr;
 }
+struct rect_v {  // a rect's planes as rtw_prim::p holds them (a0, a1, b0, b1, k)
+    double p[5];
+};
+template <int K, int A, int B>
+RTW_D void rect_arbitrate_v(const rect_v& q, int pi, const ray& r, const rect_rcp& rr, double t_min, hit_state& h) {
+    double t;
+    if (!rect_axis_rcp<K, A, B>(q, r, rr, t_min, h.t, t)) return;
+    if (better(t, pi, true, h.t, h.prim, h.rect, h.prim != -1)) {
+        h.t = t;
+        h.prim = pi;
+        h.rect = true;
+    }
+}
 RTW_D void box_arbitrate(const scene& S, int first, const ray& r, double t_min, hit_state& h) {
     const rect_rcp rr = make_rect_rcp_t(S, r, t_min);
+    // The six rects from the box's 48-B record (scene::boxes) where the scene
+    // has one (a wave-uniform test): one or two cache lines per box where the
+    // six 96-B rect records take five.  Measured (1 MI355X, A/B,
+    // profiles/r06/ab_r6v_C5.log; bit-identical, parity_r6v_boxtab.log): C5
+    // 16-spp slice 702.5 vs 679.1 Msamples/s (+3.4 %); the fp32 kernel's
+    // form (rtw_fast.h arbitrate_item) +14 %.
+    if (S.boxes) {
+        const double* b = S.boxes + 8 * (size_t)first;
+        const double x0 = b[0], x1 = b[1], y0 = b[2], y1 = b[3], z0 = b[4], z1 = b[5];
+        rect_arbitrate_v<2, 0, 1>(rect_v{{x0, x1, y0, y1, z1}}, first, r, rr, t_min, h);
+        rect_arbitrate_v<2, 0, 1>(rect_v{{x0, x1, y0, y1, z0}}, first + 1, r, rr, t_min, h);
+        rect_arbitrate_v<1, 0, 2>(rect_v{{x0, x1, z0, z1, y1}}, first + 2, r, rr, t_min, h);
+        rect_arbitrate_v<1, 0, 2>(rect_v{{x0, x1, z0, z1, y0}}, first + 3, r, rr, t_min, h);
+        rect_arbitrate_v<0, 1, 2>(rect_v{{y0, y1, z0, z1, x1}}, first + 4, r, rr, t_min, h);
+        rect_arbitrate_v<0, 1, 2>(rect_v{{y0, y1, z0, z1, x0}}, first + 5, r, rr, t_min, h);
+        return;
+    }
     rect_arbitrate_rcp<2, 0, 1>(S, first, r, rr, t_min, h);
     rect_arbitrate_rcp<2, 0, 1>(S, first + 1, r, rr, t_min, h);
     rect_arbitrate_rcp<1, 0, 2>(S, first + 2, r, rr, t_min, h);

@@ -109,6 +109,7 @@ struct fscene {
     const world_run* runs;
     const int32_t* media;
     const float* ysph;  // the y-sphere runs' pair-interleaved fp32 records (rtw_scene_upload)
+    const float* boxes;  // box items' planes, as rtwd::scene::boxes
     float light_weight;
     float mv_t0, mv_inv_den;  // the common motion interval of the y-sphere runs' movers
     int32_t n_lights, world_bvh_root, render_type, background, n_media, n_runs, n_nodes;
@@ -171,8 +172,8 @@ RTW_D bool sphere_t(const prim32& q, const fray& r, float tmin, float tmax, floa
     return t < tmax && t > tmin;
 }
 // hittable.h:149-165 / 184-200 / 241-257 (K plane axis, A / B in-plane axes)
-template <int K, int A, int B>
-RTW_D bool rect_axis_t(const prim32& q, const fray& r, float t0, float t1, float& t) {
+template <int K, int A, int B, class Q = prim32>
+RTW_D bool rect_axis_t(const Q& q, const fray& r, float t0, float t1, float& t) {
     t = (q.p[4] - comp(r.o, K)) * rcp(comp(r.d, K));
     if (t < t0 || t > t1) return false;
     const float a = __builtin_fmaf(t, comp(r.d, A), comp(r.o, A));
@@ -322,9 +323,32 @@ RTW_D void rect_arbitrate(const fscene& S, int i, const fray& r, float tmin, fhi
     float t;
     if (rect_axis_t<K, A, B>(S.prims[i], r, tmin, h.t, t) && better(t, i, true, h)) h.t = t, h.prim = i, h.rect = true;
 }
+struct rect_vf {
+    float p[5];
+};
+template <int K, int A, int B>
+RTW_D void rect_arbitrate_v(const rect_vf& q, int i, const fray& r, float tmin, fhit& h) {
+    float t;
+    if (rect_axis_t<K, A, B>(q, r, tmin, h.t, t) && better(t, i, true, h)) h.t = t, h.prim = i, h.rect = true;
+}
 RTW_D void arbitrate_item(const fscene& S, int it, const fray& r, float tmin, fhit& h) {
     if (it & RTW_ITEM_BOX) {  // a box's six rects in list order (hittable_list.h:65-114)
         const int b = it & RTW_ITEM_INDEX;
+        // the six rects from the box's 24-B record where the scene has one (a
+        // wave-uniform test; rtwd::box_arbitrate's reason): C5 fp32 32-spp
+        // slice 979 vs 862 Msamples/s (+14 %, profiles/r06/ab_r6u_C5f.log;
+        // bit-identical, parity_r6v_boxtab.log)
+        if (S.boxes) {
+            const float* q = S.boxes + 8 * (size_t)b;
+            const float x0 = q[0], x1 = q[1], y0 = q[2], y1 = q[3], z0 = q[4], z1 = q[5];
+            rect_arbitrate_v<2, 0, 1>(rect_vf{{x0, x1, y0, y1, z1}}, b, r, tmin, h);
+            rect_arbitrate_v<2, 0, 1>(rect_vf{{x0, x1, y0, y1, z0}}, b + 1, r, tmin, h);
+            rect_arbitrate_v<1, 0, 2>(rect_vf{{x0, x1, z0, z1, y1}}, b + 2, r, tmin, h);
+            rect_arbitrate_v<1, 0, 2>(rect_vf{{x0, x1, z0, z1, y0}}, b + 3, r, tmin, h);
+            rect_arbitrate_v<0, 1, 2>(rect_vf{{y0, y1, z0, z1, x1}}, b + 4, r, tmin, h);
+            rect_arbitrate_v<0, 1, 2>(rect_vf{{y0, y1, z0, z1, x0}}, b + 5, r, tmin, h);
+            return;
+        }
         rect_arbitrate<2, 0, 1>(S, b, r, tmin, h);
         rect_arbitrate<2, 0, 1>(S, b + 1, r, tmin, h);
         rect_arbitrate<1, 0, 2>(S, b + 2, r, tmin, h);
@@ -439,7 +463,18 @@ RTW_D void group_bvh(const fscene& S, int root, const fray& r, float tmin, fhit&
         const bvh_node32 nd = node_at<PALL>(S, stk.at(--sp));
         if (!slab(nd, sr, t0, h.t)) continue;
         if (nd.b < 0) {
-            for (int k = 0; k < -nd.b; ++k) arbitrate_item(S, S.items[nd.a + k], r, tmin, h);
+            // (the fp32 node copy: b == -1 one item, in a; b < -16 two items,
+            // a and b's low bits; else an index and a count)
+            const bool inl = nd.b == -1 || nd.b < -16;
+            const int n = nd.b == -1 ? 1 : (nd.b < -16 ? 2 : -nd.b);
+            for (int k = 0; k < n; ++k) {
+                int it;
+                if (inl)
+                    it = k == 0 ? nd.a : (nd.b & 0x7fffffff);
+                else
+                    it = S.items[nd.a + k];
+                arbitrate_item(S, it, r, tmin, h);
+            }
         } else if (sp + 2 <= STK::cap) {
             stk.at(sp++) = nd.b & 0x0fffffff;
             stk.at(sp++) = nd.a;

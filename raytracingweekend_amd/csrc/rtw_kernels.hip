@@ -2073,13 +2073,16 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     // a BVH whose bounds are not finite within 2^90 is not used at all (the
     // flat list gives the same image)
     std::vector<bvh_node32> dnodes32(dnodes.size());
-    // The fp32 kernels' copy of the nodes: a one-item leaf of the world BVH
-    // holds its item (entry or ~prim) in a instead of its index into the
-    // item array, so the fp32 world walk (rtw_fast.h world_closest) reaches
-    // the prim with one dependent load less per leaf.  Measured (1 MI355X,
-    // A/B, profiles/r06/ab_r6r_C3f.log; bit-identical, parity_r6r_inl2.log):
-    // C3 fp32 +1.9 %.  The fp64 walks keep the shared form: the same inline
-    // leaves there measured C3 -0.7 % (ab_r6r_C3.log).
+    // The fp32 kernels' copy of the nodes: a one-item leaf holds its item
+    // (entry, ~prim, prim or box) in a instead of its index into the item
+    // array (b = -1), and a two-item group leaf holds both (a, and b =
+    // INT_MIN | second; b in [-16, -2] stays an index and a count), so the
+    // fp32 walks (rtw_fast.h) reach the prims with one dependent load less
+    // per leaf.  Measured (1 MI355X, A/B; bit-identical): C3 fp32 +1.9 %
+    // (profiles/r06/ab_r6r_C3f.log, parity_r6r_inl2.log), C5 fp32 +0.5 % for
+    // the group pairs (ab_r6t_C5f.log, parity_r6t_pair.log).  The fp64 walks
+    // keep the shared form: inline leaves there measured C3 -0.7 %
+    // (ab_r6r_C3.log).
     std::vector<bvh_node32> dnodes32f(dnodes.size());
     double bvh_bound = 0.0;
     bool bvh_ok = dnodes.size() < (1u << 28);
@@ -2098,7 +2101,13 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         M.a = N.left;
         M.b = N.count > 0 ? -N.count : (N.right | (N.pad << 28));
         dnodes32f[k] = M;
-        if (world_node[k] && N.count == 1) dnodes32f[k].a = ditems[N.left];
+        if (N.count == 1) dnodes32f[k].a = ditems[N.left];
+        // a group leaf's two items (prims or boxes: >= 0) in a and b's low bits
+        if (!world_node[k] && N.count == 2 && ditems[N.left] >= 0 && ditems[N.left + 1] >= 0 &&
+            ditems[N.left + 1] < 0x7fffffef) {
+            dnodes32f[k].a = ditems[N.left];
+            dnodes32f[k].b = (int32_t)(0x80000000u | (uint32_t)ditems[N.left + 1]);
+        }
     }
     // Breadth-first numbering from all roots together (the world BVH's, then
     // every group's, in entry order): nodes [0, k) are then the top levels of
@@ -2158,6 +2167,42 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             dev_ops.push_back(o);
         }
     }
+    // Box items' planes (scene::boxes): {x0, x1, y0, y1, z0, z1} per box, at
+    // its first rect's index, when every box item's six rects are the
+    // hittable_list box's (+z, -z, +y, -y, +x, -x: XY at z1 and z0, XZ at y1
+    // and y0, YZ at x1 and x0, each with the box's other two ranges) to the
+    // last bit; otherwise none, and the walks read the rects.
+    // (RTW_BOX_TABLE=0 at upload: no table, for tests of the rect path)
+    std::vector<int> box_firsts;
+    const char* box_env = std::getenv("RTW_BOX_TABLE");
+    const bool box_table = !(box_env && *box_env && std::atoi(box_env) == 0);
+    for (int32_t it : ditems)
+        if (box_table && it >= 0 && (it & RTW_ITEM_BOX)) box_firsts.push_back(it & RTW_ITEM_INDEX);
+    auto box_planes = [&](auto get, int i, auto* out) {  // get(prim, k) = p[k]; false if not a box
+        if (i < 0 || i + 6 > (int)dprims.size()) return false;
+        const int ty[6] = {RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XZ,
+                           RTW_PRIM_RECT_XZ, RTW_PRIM_RECT_YZ, RTW_PRIM_RECT_YZ};
+        for (int j = 0; j < 6; ++j)
+            if (dprims[i + j].type != ty[j]) return false;
+        const auto x0 = get(i + 5, 4), x1 = get(i + 4, 4), y0 = get(i + 3, 4), y1 = get(i + 2, 4);
+        const auto z0 = get(i + 1, 4), z1 = get(i, 4);
+        const decltype(x0) want[6][4] = {{x0, x1, y0, y1}, {x0, x1, y0, y1}, {x0, x1, z0, z1},
+                                         {x0, x1, z0, z1}, {y0, y1, z0, z1}, {y0, y1, z0, z1}};
+        for (int j = 0; j < 6; ++j)
+            for (int k = 0; k < 4; ++k)
+                if (!(get(i + j, k) == want[j][k])) return false;
+        out[0] = x0, out[1] = x1, out[2] = y0, out[3] = y1, out[4] = z0, out[5] = z1;
+        return true;
+    };
+    std::vector<double> boxes64;
+    if (!box_firsts.empty()) {
+        boxes64.assign(8 * dprims.size(), 0.0);
+        for (int i : box_firsts)
+            if (!box_planes([&](int q, int k) { return dprims[q].p[k]; }, i, boxes64.data() + 8 * (size_t)i)) {
+                boxes64.clear();
+                break;
+            }
+    }
     std::vector<part> parts = {
         // parts 0..10 are what shading reads; they come first so a small
         // scene's shading data is one contiguous prefix the shade kernel can
@@ -2177,6 +2222,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         {ditems.data(), sizeof(int32_t) * ditems.size(), 0},
         {runs.data(), sizeof(world_run) * runs.size(), 0},
         {ysph.data(), sizeof(float) * ysph.size(), 0},
+        {boxes64.data(), sizeof(double) * boxes64.size(), 0},
     };
     size_t total = 0;
     for (auto& p : parts) {
@@ -2208,6 +2254,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
     S.items = (const int32_t*)at(12);
     S.runs = (const world_run*)at(13);
     S.ysph = (const float*)at(14);
+    S.boxes = (const double*)at(15);
     S.ysb_cx = ysb[0], S.ysb_cy = ysb[1], S.ysb_dy = ysb[2], S.ysb_cz = ysb[3], S.ysb_r2 = ysb[4];
     S.n_runs = (int32_t)runs.size();
     S.mv_common = mv_common ? 1 : 0;
@@ -2353,6 +2400,15 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             o.type = T.type, o.odd = T.odd, o.even = T.even, o.scale = (float)T.scale;
             for (int j = 0; j < 3; ++j) o.color[j] = (float)T.color[j];
         }
+        std::vector<float> boxes32;  // box planes in fp32 (fscene::boxes)
+        if (!boxes64.empty()) {
+            boxes32.assign(8 * p32.size(), 0.0f);
+            for (int i : box_firsts)
+                if (!box_planes([&](int q, int k) { return p32[q].p[k]; }, i, boxes32.data() + 8 * (size_t)i)) {
+                    boxes32.clear();
+                    break;
+                }
+        }
         std::vector<float> rv32(d->has_perlin ? 768 : 0), fr32(frames.size());
         for (size_t k = 0; k < rv32.size(); ++k) rv32[k] = (float)d->perlin_ranvec[k];
         for (size_t k = 0; k < frames.size(); ++k) fr32[k] = (float)frames[k];
@@ -2370,6 +2426,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             {d->has_perlin ? d->perlin_perm : nullptr, d->has_perlin ? sizeof(int32_t) * 768 : 0, 0},
             // (after the staged prefix)
             {dnodes32f.data(), sizeof(bvh_node32) * dnodes32f.size(), 0},
+            {boxes32.data(), sizeof(float) * boxes32.size(), 0},
         };
         size_t tot = 0;
         for (auto& x : p2) {
@@ -2394,6 +2451,7 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
         F.perm = p2[8].bytes ? (const int32_t*)(b2 + p2[8].off) : nullptr;
         h->f32_bytes = (uint32_t)(p2[8].off + p2[8].bytes);
         F.nodes = S.nodes ? (const node_store*)(b2 + p2[9].off) : nullptr;
+        F.boxes = p2[10].bytes ? (const float*)(b2 + p2[10].off) : nullptr;
         F.items = S.items;
         F.runs = S.runs;
         F.media = S.media;

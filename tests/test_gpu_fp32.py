@@ -142,6 +142,21 @@ def test_node_packet_changes_no_sample(gpu, scene, precision):
     assert np.all(np.isfinite(with_p)) and with_p.sum() > 0
 
 
+@pytest.mark.parametrize("bvh", [True, False])
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_box_table_changes_no_sample(gpu, bvh, precision):
+    """Box items read their six rects from one planes record (scene::boxes,
+    rtw_scene_upload, when every box's rects match the box's planes): the
+    Book-2 render with the table equals the render that reads the rects
+    (RTW_BOX_TABLE=0) bit for bit, with the same traversal count -- in the
+    group-BVH walks (bvh) and with the flat list, which has no box items."""
+    nx, ny, spp, depth = 96, 64, 4, 50
+    with_t, s1 = _render_child({}, "book2_final", nx, ny, spp, depth, 11, bvh, precision)
+    without, s0 = _render_child({"RTW_BOX_TABLE": "0"}, "book2_final", nx, ny, spp, depth, 11, bvh, precision)
+    assert s1 == s0 and np.array_equal(with_t, without)
+    assert np.all(np.isfinite(with_t)) and with_t.sum() > 0
+
+
 def test_cli_precision_switch(tmp_path):
     """The reference-main equivalent (rtw_render) renders in either precision
     (--precision fp64|fp32, SURVEY.md §5's config row) and writes its PPM."""
