@@ -373,9 +373,10 @@ struct scene {
     // and r^2 of the filtered spheres
     const float* ysph;
     float ysb_cx, ysb_cy, ysb_dy, ysb_cz, ysb_r2;
-    // box items' planes: for the first rect i of a box, {x0, x1, y0, y1, z0,
-    // z1} at boxes[8 i] (rtw_scene_upload, when every box's six rects match
-    // them; nullptr: the walks read the rects)
+    // box items' planes: per box item a 64-B record {x0, x1, y0, y1, z0, z1,
+    // first rect (int)}, the items then RTW_ITEM_BOX | record
+    // (rtw_scene_upload, when every box's six rects match them; nullptr: the
+    // items are RTW_ITEM_BOX | first rect and the walks read the rects)
     const double* boxes;
     // BVH node packets staged in LDS: the upload numbers the nodes of every
     // BVH breadth-first from all roots together, so nodes [0, n_lnodes) are
@@ -976,17 +977,21 @@ RTW_D void rect_arbitrate_v(const rect_v& q, int pi, const ray& r, const rect_rc
         h.rect = true;
     }
 }
-RTW_D void box_arbitrate(const scene& S, int first, const ray& r, double t_min, hit_state& h) {
+RTW_D void box_arbitrate(const scene& S, int idx, const ray& r, double t_min, hit_state& h) {
     const rect_rcp rr = make_rect_rcp_t(S, r, t_min);
-    // The six rects from the box's 48-B record (scene::boxes) where the scene
-    // has one (a wave-uniform test): one or two cache lines per box where the
-    // six 96-B rect records take five.  Measured (1 MI355X, A/B,
-    // profiles/r06/ab_r6v_C5.log; bit-identical, parity_r6v_boxtab.log): C5
-    // 16-spp slice 702.5 vs 679.1 Msamples/s (+3.4 %); the fp32 kernel's
-    // form (rtw_fast.h arbitrate_item) +14 %.
+    // The six rects from the box's 64-B record (scene::boxes) where the scene
+    // has one (a wave-uniform test): one cache line per box where the six
+    // 96-B rect records take five.  Measured (1 MI355X, A/B; bit-identical):
+    // C5 16-spp slice 702.5 vs 679.1 Msamples/s (+3.4 %), the fp32 kernel's
+    // form (rtw_fast.h arbitrate_item) +14 % (profiles/r06/ab_r6v_C5.log,
+    // ab_r6u_C5f.log, parity_r6v_boxtab.log, records at the first rect's
+    // index); the records packed densely, the 400 ground boxes in 25 KB
+    // (12.5 KB in fp32) instead of spread over 150 KB: +0.8 % / +0.4 %
+    // (ab_r6dn_*.log, parity_r6dn.log).
     if (S.boxes) {
-        const double* b = S.boxes + 8 * (size_t)first;
+        const double* b = S.boxes + 8 * (size_t)idx;  // record idx
         const double x0 = b[0], x1 = b[1], y0 = b[2], y1 = b[3], z0 = b[4], z1 = b[5];
+        const int first = *reinterpret_cast<const int32_t*>(b + 6);
         rect_arbitrate_v<2, 0, 1>(rect_v{{x0, x1, y0, y1, z1}}, first, r, rr, t_min, h);
         rect_arbitrate_v<2, 0, 1>(rect_v{{x0, x1, y0, y1, z0}}, first + 1, r, rr, t_min, h);
         rect_arbitrate_v<1, 0, 2>(rect_v{{x0, x1, z0, z1, y1}}, first + 2, r, rr, t_min, h);
@@ -995,6 +1000,7 @@ RTW_D void box_arbitrate(const scene& S, int first, const ray& r, double t_min, 
         rect_arbitrate_v<0, 1, 2>(rect_v{{y0, y1, z0, z1, x0}}, first + 5, r, rr, t_min, h);
         return;
     }
+    const int first = idx;  // (no table: the item names the first rect)
     rect_arbitrate_rcp<2, 0, 1>(S, first, r, rr, t_min, h);
     rect_arbitrate_rcp<2, 0, 1>(S, first + 1, r, rr, t_min, h);
     rect_arbitrate_rcp<1, 0, 2>(S, first + 2, r, rr, t_min, h);

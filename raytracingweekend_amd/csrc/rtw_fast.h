@@ -334,19 +334,20 @@ RTW_D void rect_arbitrate_v(const rect_vf& q, int i, const fray& r, float tmin, 
 RTW_D void arbitrate_item(const fscene& S, int it, const fray& r, float tmin, fhit& h) {
     if (it & RTW_ITEM_BOX) {  // a box's six rects in list order (hittable_list.h:65-114)
         const int b = it & RTW_ITEM_INDEX;
-        // the six rects from the box's 24-B record where the scene has one (a
+        // the six rects from the box's 32-B record where the scene has one (a
         // wave-uniform test; rtwd::box_arbitrate's reason): C5 fp32 32-spp
         // slice 979 vs 862 Msamples/s (+14 %, profiles/r06/ab_r6u_C5f.log;
         // bit-identical, parity_r6v_boxtab.log)
-        if (S.boxes) {
+        if (S.boxes) {  // (b is the record; the record names the first rect)
             const float* q = S.boxes + 8 * (size_t)b;
             const float x0 = q[0], x1 = q[1], y0 = q[2], y1 = q[3], z0 = q[4], z1 = q[5];
-            rect_arbitrate_v<2, 0, 1>(rect_vf{{x0, x1, y0, y1, z1}}, b, r, tmin, h);
-            rect_arbitrate_v<2, 0, 1>(rect_vf{{x0, x1, y0, y1, z0}}, b + 1, r, tmin, h);
-            rect_arbitrate_v<1, 0, 2>(rect_vf{{x0, x1, z0, z1, y1}}, b + 2, r, tmin, h);
-            rect_arbitrate_v<1, 0, 2>(rect_vf{{x0, x1, z0, z1, y0}}, b + 3, r, tmin, h);
-            rect_arbitrate_v<0, 1, 2>(rect_vf{{y0, y1, z0, z1, x1}}, b + 4, r, tmin, h);
-            rect_arbitrate_v<0, 1, 2>(rect_vf{{y0, y1, z0, z1, x0}}, b + 5, r, tmin, h);
+            const int f = *reinterpret_cast<const int32_t*>(q + 6);
+            rect_arbitrate_v<2, 0, 1>(rect_vf{{x0, x1, y0, y1, z1}}, f, r, tmin, h);
+            rect_arbitrate_v<2, 0, 1>(rect_vf{{x0, x1, y0, y1, z0}}, f + 1, r, tmin, h);
+            rect_arbitrate_v<1, 0, 2>(rect_vf{{x0, x1, z0, z1, y1}}, f + 2, r, tmin, h);
+            rect_arbitrate_v<1, 0, 2>(rect_vf{{x0, x1, z0, z1, y0}}, f + 3, r, tmin, h);
+            rect_arbitrate_v<0, 1, 2>(rect_vf{{y0, y1, z0, z1, x1}}, f + 4, r, tmin, h);
+            rect_arbitrate_v<0, 1, 2>(rect_vf{{y0, y1, z0, z1, x0}}, f + 5, r, tmin, h);
             return;
         }
         rect_arbitrate<2, 0, 1>(S, b, r, tmin, h);

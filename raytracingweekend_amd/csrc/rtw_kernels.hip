@@ -2052,6 +2052,59 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             }
         }
     }
+    // Box items' planes (scene::boxes): one 64-B record per box item,
+    // {x0, x1, y0, y1, z0, z1, first rect (int)}, packed densely (the 400
+    // ground boxes of Book 2 in 25 KB), when every box item's six rects are
+    // the hittable_list box's (+z, -z, +y, -y, +x, -x: XY at z1 and z0, XZ at
+    // y1 and y0, YZ at x1 and x0, each with the box's other two ranges) to
+    // the last bit.  The device items then read RTW_ITEM_BOX | record (the
+    // fp32 copy likewise, fscene::boxes); otherwise no table, and the walks
+    // read the rects of RTW_ITEM_BOX | first rect.
+    // (RTW_BOX_TABLE=0 at upload: no table, for tests of the rect path)
+    const char* box_env = std::getenv("RTW_BOX_TABLE");
+    const bool box_table = !(box_env && *box_env && std::atoi(box_env) == 0);
+    auto box_planes = [&](auto get, int i, auto* out) {  // get(prim, k) = p[k]; false if not a box
+        if (i < 0 || i + 6 > (int)dprims.size()) return false;
+        const int ty[6] = {RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XZ,
+                           RTW_PRIM_RECT_XZ, RTW_PRIM_RECT_YZ, RTW_PRIM_RECT_YZ};
+        for (int j = 0; j < 6; ++j)
+            if (dprims[i + j].type != ty[j]) return false;
+        const auto x0 = get(i + 5, 4), x1 = get(i + 4, 4), y0 = get(i + 3, 4), y1 = get(i + 2, 4);
+        const auto z0 = get(i + 1, 4), z1 = get(i, 4);
+        const decltype(x0) want[6][4] = {{x0, x1, y0, y1}, {x0, x1, y0, y1}, {x0, x1, z0, z1},
+                                         {x0, x1, z0, z1}, {y0, y1, z0, z1}, {y0, y1, z0, z1}};
+        for (int j = 0; j < 6; ++j)
+            for (int k = 0; k < 4; ++k)
+                if (!(get(i + j, k) == want[j][k])) return false;
+        out[0] = x0, out[1] = x1, out[2] = y0, out[3] = y1, out[4] = z0, out[5] = z1;
+        int32_t f = i;
+        std::memcpy(out + 6, &f, sizeof f);  // the first rect, in the record's seventh slot
+        return true;
+    };
+    std::vector<int> box_firsts;  // record -> first rect
+    std::vector<double> boxes64;
+    {
+        std::vector<int> slot_items;  // item slots of box items
+        for (size_t k = 0; k < ditems.size(); ++k)
+            if (box_table && ditems[k] >= 0 && (ditems[k] & RTW_ITEM_BOX)) slot_items.push_back((int)k);
+        std::map<int, int> rec_of;
+        bool ok = true;
+        for (int k : slot_items) {
+            const int i = ditems[k] & RTW_ITEM_INDEX;
+            if (rec_of.count(i)) continue;
+            rec_of[i] = (int)box_firsts.size();
+            box_firsts.push_back(i);
+        }
+        boxes64.assign(8 * box_firsts.size(), 0.0);
+        for (size_t b = 0; b < box_firsts.size() && ok; ++b)
+            ok = box_planes([&](int q, int k) { return dprims[q].p[k]; }, box_firsts[b], boxes64.data() + 8 * b);
+        if (!ok) {
+            boxes64.clear();
+            box_firsts.clear();
+        } else {
+            for (int k : slot_items) ditems[k] = RTW_ITEM_BOX | rec_of[ditems[k] & RTW_ITEM_INDEX];
+        }
+    }
     // Inner BVH nodes: the axis along which their children's centres differ
     // most, and whether the left child is the upper one (push_children).
     std::vector<rtw_bvh_node> dnodes(d->bvh_nodes, d->bvh_nodes + d->n_bvh_nodes);
@@ -2166,42 +2219,6 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             for (int j = 0; j < 3; ++j) o.p[j] = E.op_param[k][j];
             dev_ops.push_back(o);
         }
-    }
-    // Box items' planes (scene::boxes): {x0, x1, y0, y1, z0, z1} per box, at
-    // its first rect's index, when every box item's six rects are the
-    // hittable_list box's (+z, -z, +y, -y, +x, -x: XY at z1 and z0, XZ at y1
-    // and y0, YZ at x1 and x0, each with the box's other two ranges) to the
-    // last bit; otherwise none, and the walks read the rects.
-    // (RTW_BOX_TABLE=0 at upload: no table, for tests of the rect path)
-    std::vector<int> box_firsts;
-    const char* box_env = std::getenv("RTW_BOX_TABLE");
-    const bool box_table = !(box_env && *box_env && std::atoi(box_env) == 0);
-    for (int32_t it : ditems)
-        if (box_table && it >= 0 && (it & RTW_ITEM_BOX)) box_firsts.push_back(it & RTW_ITEM_INDEX);
-    auto box_planes = [&](auto get, int i, auto* out) {  // get(prim, k) = p[k]; false if not a box
-        if (i < 0 || i + 6 > (int)dprims.size()) return false;
-        const int ty[6] = {RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XY, RTW_PRIM_RECT_XZ,
-                           RTW_PRIM_RECT_XZ, RTW_PRIM_RECT_YZ, RTW_PRIM_RECT_YZ};
-        for (int j = 0; j < 6; ++j)
-            if (dprims[i + j].type != ty[j]) return false;
-        const auto x0 = get(i + 5, 4), x1 = get(i + 4, 4), y0 = get(i + 3, 4), y1 = get(i + 2, 4);
-        const auto z0 = get(i + 1, 4), z1 = get(i, 4);
-        const decltype(x0) want[6][4] = {{x0, x1, y0, y1}, {x0, x1, y0, y1}, {x0, x1, z0, z1},
-                                         {x0, x1, z0, z1}, {y0, y1, z0, z1}, {y0, y1, z0, z1}};
-        for (int j = 0; j < 6; ++j)
-            for (int k = 0; k < 4; ++k)
-                if (!(get(i + j, k) == want[j][k])) return false;
-        out[0] = x0, out[1] = x1, out[2] = y0, out[3] = y1, out[4] = z0, out[5] = z1;
-        return true;
-    };
-    std::vector<double> boxes64;
-    if (!box_firsts.empty()) {
-        boxes64.assign(8 * dprims.size(), 0.0);
-        for (int i : box_firsts)
-            if (!box_planes([&](int q, int k) { return dprims[q].p[k]; }, i, boxes64.data() + 8 * (size_t)i)) {
-                boxes64.clear();
-                break;
-            }
     }
     std::vector<part> parts = {
         // parts 0..10 are what shading reads; they come first so a small
@@ -2400,15 +2417,10 @@ int upload_scene(handle_t* h, const rtw_scene_desc* d) {
             o.type = T.type, o.odd = T.odd, o.even = T.even, o.scale = (float)T.scale;
             for (int j = 0; j < 3; ++j) o.color[j] = (float)T.color[j];
         }
-        std::vector<float> boxes32;  // box planes in fp32 (fscene::boxes)
-        if (!boxes64.empty()) {
-            boxes32.assign(8 * p32.size(), 0.0f);
-            for (int i : box_firsts)
-                if (!box_planes([&](int q, int k) { return p32[q].p[k]; }, i, boxes32.data() + 8 * (size_t)i)) {
-                    boxes32.clear();
-                    break;
-                }
-        }
+        std::vector<float> boxes32(8 * box_firsts.size(), 0.0f);  // the same records in fp32 (fscene::boxes)
+        for (size_t b = 0; b < box_firsts.size(); ++b)
+            if (!box_planes([&](int q, int k) { return p32[q].p[k]; }, box_firsts[b], boxes32.data() + 8 * b))
+                return rtw_fail(RTW_ERR_INVALID, "box planes: fp32 rects differ from the fp64 ones");
         std::vector<float> rv32(d->has_perlin ? 768 : 0), fr32(frames.size());
         for (size_t k = 0; k < rv32.size(); ++k) rv32[k] = (float)d->perlin_ranvec[k];
         for (size_t k = 0; k < frames.size(); ++k) fr32[k] = (float)frames[k];
